@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""bench.py - headline benchmark of the MI355X CKKS engine.
+
+Metric (BASELINE.json): ct x ct + relinearization (+ rescale) per second at
+N = 2^16, L = 8 RNS primes (configs[2]: batch = 256 ciphertext pairs per GPU,
+one step = one batch through he_mul_rescale_batch).  Inputs are synthetic
+random-residue ciphertexts already resident in HBM (poly_fill_uniform,
+splitmix64 streams); the relinearization key is a real key (he_genrlk).
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL), each rank
+multiplies its own batch (independent ciphertexts: no data-path
+collective); the collective is only the barrier / max-time reduction.
+`value` = pairs processed by all ranks / max rank time ("scaling": "weak").
+
+Also reported on rank 0:
+  roofline      - for the dominant kernel, algorithmic bytes per launch /
+                  its average launch duration (HIP events on the engine
+                  stream, same shapes as inside the step), vs 8 TB/s;
+  cpu_baseline  - the CPU restatement (oracle/, "port") timed on this host
+                  on a bounded sample of the same op;
+  op_roofline   - the whole op against its algorithmic bytes (24.4 MB/op).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--logn", type=int, default=16)
+    ap.add_argument("--nlimbs", type=int, default=8)
+    ap.add_argument("--dnum", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-ops", type=int, default=0, help="CPU sample size (default: 4 per thread)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from hectr_amd.gpqhe import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    L, logn, B = args.nlimbs, args.logn, args.batch
+    n = 1 << logn
+    dnum = args.dnum or L
+    eng = Engine.product()
+    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=60, qi_bits=50, p_bits=60,
+                    seed=1000 + rank)
+    stream = torch.cuda.Stream()
+    eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
+    pk, sk, rlk = eng.pk(), eng.sk(), eng.evk()
+    eng.keypair(pk, sk)
+    eng.genrlk(rlk, sk)
+    K = eng.K
+    in_words, out_words = 2 * L * n, 2 * (L - 1) * n
+    a = torch.empty(B * in_words, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    out = torch.empty(B * out_words, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    eng.lib.poly_fill_uniform(a.data_ptr(), 2 * B, L, 11 + 2 * rank)
+    eng.lib.poly_fill_uniform(b.data_ptr(), 2 * B, L, 12 + 2 * rank)
+    eng.sync()
+
+    def step():
+        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    eng.sync()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    ev_s = ev0.elapsed_time(ev1) / 1e3
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ops = world * B * args.steps
+    value = ops / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # algorithmic bytes per op: 2 ct in, 1 ct out at L-1, rlk amortised over the batch
+    evk_bytes = 2 * eng.info.dnum * (L + K) * n * 8
+    alg_bytes = (2 * in_words + out_words) * 8 + evk_bytes / B
+
+    result = None
+    if rank == 0:
+        from hectr_amd import kprof
+        dom = kprof.dominant_kernel(eng, B=min(B, 64), L=L, logn=logn)
+        result = {
+            "metric": "ct×ct+relin/sec at N=2^16, L=8 RNS primes; encrypted CSTR-MPC steps/sec",
+            "value": value,
+            "unit": "ct-mult/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic random-residue ciphertexts (splitmix64), real relinearization key",
+            "config": {"workload": f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, "
+                                   f"dnum={eng.info.dnum}, batch={B} pairs per GPU",
+                       "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": K,
+                       "dnum": eng.info.dnum, "parallelism": f"batch-sharded x{world}"},
+            "event_s_rank0": ev_s,
+            "op_roofline": {"alg_bytes_per_op": alg_bytes,
+                            "achieved_GBs": alg_bytes * value / world / 1e9,
+                            "frac": alg_bytes * value / world / 1e9 / HBM_PEAK_GBS},
+            "roofline": dom,
+        }
+    barrier()
+    if rank == 0 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, logn, L, dnum)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, logn, L, dnum):
+    """Oracle (CPU restatement, -O3, OpenMP over the batch) on a bounded
+    sample of the same op; threads = OMP_NUM_THREADS (16 on the GPU box)."""
+    import numpy as np
+
+    from hectr_amd.gpqhe import Engine
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    ora = Engine.oracle()
+    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=60, qi_bits=50, p_bits=60, seed=7)
+    pk, sk, rlk = ora.pk(), ora.sk(), ora.evk()
+    ora.keypair(pk, sk)
+    ora.genrlk(rlk, sk)
+    n = 1 << logn
+    cnt = args.cpu_ops or max(8, 4 * threads)
+    a = np.zeros(cnt * 2 * L * n, dtype=np.uint64)
+    b = np.zeros_like(a)
+    out = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
+    ora.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 11)
+    ora.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 12)
+    t0 = time.perf_counter()
+    ora.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk))
+    dt = time.perf_counter() - t0
+    ora.exit()
+    return {"value": cnt / dt, "unit": "ct-mult/s", "cores": threads, "kind": "port",
+            "sample": f"{cnt} ct x ct+relin+rescale ops at N=2^{logn}, L={L} ({dt:.1f} s)"}
+
+
+if __name__ == "__main__":
+    main()

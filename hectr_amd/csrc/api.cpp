@@ -1,0 +1,981 @@
+// api.cpp - the he_* / hectx_* C ABI of libgpqhe.so (include/gpqhe.h) on
+// MI355X.  Host C++ orchestrating the gfx950 kernels of kernels.hip on one
+// HIP stream; every object payload lives in HBM.  Call-site contract:
+// reference src/ctr.c:445-618 and src/hempc.c:216-274 (see gpqhe.h).
+#include "gpqhe_internal.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <unordered_map>
+
+Context G;
+
+// ===========================================================================
+// Device memory pool: exact-size free lists, stream-ordered reuse.
+// ===========================================================================
+static std::map<size_t, std::vector<void *>> g_free;
+static std::unordered_map<void *, size_t> g_size;
+
+static size_t pool_round(size_t b)
+{
+  return (b + 4095) & ~(size_t)4095;
+}
+
+void *pool_alloc(size_t bytes)
+{
+  const size_t b = pool_round(bytes ? bytes : 1);
+  auto it = g_free.find(b);
+  if (it != g_free.end() && !it->second.empty()) {
+    void *p = it->second.back();
+    it->second.pop_back();
+    return p;
+  }
+  void *p = nullptr;
+  hipError_t e = hipMalloc(&p, b);
+  if (e != hipSuccess) {
+    // give cached blocks back and retry once
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+    for (auto &kv : g_free)
+      for (void *q : kv.second) {
+        (void)hipFree(q);
+        g_size.erase(q);
+      }
+    g_free.clear();
+    HIP_CHECK(hipMalloc(&p, b));
+  }
+  g_size[p] = b;
+  return p;
+}
+
+void pool_free(void *p)
+{
+  if (!p)
+    return;
+  auto it = g_size.find(p);
+  if (it == g_size.end())
+    return;  // payload of an object that outlived a previous context (already released)
+  g_free[it->second].push_back(p);
+}
+
+void pool_release_all()
+{
+  // g_size holds every block ever allocated (free-listed or still owned by a
+  // caller object that outlives the context); free each exactly once
+  for (auto &kv : g_size)
+    HIP_CHECK(hipFree(kv.first));
+  g_size.clear();
+  g_free.clear();
+}
+
+// RAII workspace
+struct Ws {
+  uint64_t *p;
+  explicit Ws(size_t words) : p((uint64_t *)pool_alloc(words * 8)) {}
+  ~Ws() { pool_free(p); }
+  Ws(const Ws &) = delete;
+  Ws &operator=(const Ws &) = delete;
+};
+
+// Pinned staging ring for small host->device uploads (encode).
+struct Stage {
+  void *host = nullptr;
+  hipEvent_t ev = nullptr;
+  size_t bytes = 0;
+};
+static Stage g_stage[8];
+static unsigned g_stage_next = 0;
+
+static void upload(void *dst, const void *src, size_t bytes)
+{
+  Stage &s = g_stage[g_stage_next++ % 8];
+  if (s.ev)
+    HIP_CHECK(hipEventSynchronize(s.ev));
+  else
+    HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  if (s.bytes < bytes) {
+    if (s.host)
+      HIP_CHECK(hipHostFree(s.host));
+    HIP_CHECK(hipHostMalloc(&s.host, bytes, hipHostMallocDefault));
+    s.bytes = bytes;
+  }
+  memcpy(s.host, src, bytes);
+  HIP_CHECK(hipMemcpyAsync(dst, s.host, bytes, hipMemcpyHostToDevice, G.stream));
+  HIP_CHECK(hipEventRecord(s.ev, G.stream));
+}
+
+static void stage_release()
+{
+  for (Stage &s : g_stage) {
+    if (s.ev) {
+      (void)hipEventSynchronize(s.ev);
+      (void)hipEventDestroy(s.ev);
+    }
+    if (s.host)
+      (void)hipHostFree(s.host);
+    s = Stage{};
+  }
+}
+
+// ===========================================================================
+// Helpers
+// ===========================================================================
+static void check_ctx()
+{
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
+}
+
+static inline he_ct_t *OB(void *o) { return (he_ct_t *)o; }
+static inline const he_ct_t *OB(const void *o) { return (const he_ct_t *)o; }
+
+static inline uint64_t *limb(const void *vo, unsigned p, unsigned l)
+{
+  const he_ct_t *o = OB(vo);
+  return o->data + (((size_t)p * o->cap + l) << G.logn);
+}
+
+static inline size_t pstride(const void *vo)
+{
+  return (size_t)OB(vo)->cap << G.logn;
+}
+
+static LimbSet limbset(uint64_t *base, const unsigned *mods, unsigned per, unsigned groups, size_t stride)
+{
+  LimbSet s{};
+  s.base = base;
+  s.per = per;
+  s.count = per * groups;
+  s.stride = stride;
+  for (unsigned i = 0; i < per; i++)
+    s.mods[i] = (uint8_t)mods[i];
+  return s;
+}
+
+static LimbSet qlimbs(uint64_t *base, unsigned lvl, unsigned groups, size_t stride)
+{
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned i = 0; i < lvl; i++)
+    mods[i] = i;
+  return limbset(base, mods, lvl, groups, stride);
+}
+
+static unsigned basis_qp(unsigned lvl, unsigned *mods)
+{
+  for (unsigned t = 0; t < lvl; t++)
+    mods[t] = t;
+  for (unsigned k = 0; k < G.K; k++)
+    mods[lvl + k] = G.L + k;
+  return lvl + G.K;
+}
+
+static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
+{
+  check_ctx();
+  he_ct_t *o = OB(vo);
+  memset(o, 0, sizeof(*o));
+  o->npoly = npoly;
+  o->cap = cap;
+  const size_t bytes = ((size_t)npoly * cap << G.logn) * 8;
+  o->data = (uint64_t *)pool_alloc(bytes);
+  HIP_CHECK(hipMemsetAsync(o->data, 0, bytes, G.stream));
+}
+
+static void obj_free(void *vo)
+{
+  he_ct_t *o = OB(vo);
+  if (o->data && G.init)
+    pool_free(o->data);
+  memset(o, 0, sizeof(*o));
+}
+
+static uint64_t next_stream()
+{
+  return G.counter++;
+}
+
+static void sample_small_ntt(uint64_t *dst, const unsigned *mods, unsigned nm, int cbd)
+{
+  LimbSet s = limbset(dst, mods, nm, 1, (size_t)nm << G.logn);
+  k_sample_small(s, next_stream(), cbd);
+  k_ntt(s, false);
+}
+
+static void sample_uniform(uint64_t *dst, const unsigned *mods, unsigned nm)
+{
+  LimbSet s = limbset(dst, mods, nm, 1, (size_t)nm << G.logn);
+  k_sample_uniform(s, next_stream());
+}
+
+// ===========================================================================
+// MPI
+// ===========================================================================
+struct gpqhe_mpi {
+  unsigned nwords;
+  uint64_t w[64];
+};
+
+extern "C" MPI gpqhe_mpi_set_ui(MPI w, unsigned long u)
+{
+  if (!w)
+    w = (MPI)calloc(1, sizeof(*w));
+  memset(w->w, 0, sizeof(w->w));
+  w->w[0] = u;
+  w->nwords = 1;
+  return w;
+}
+
+extern "C" void gpqhe_mpi_lshift(MPI x, MPI a, unsigned int n)
+{
+  uint64_t src[64], dst[64];
+  memcpy(src, a->w, sizeof(src));
+  memset(dst, 0, sizeof(dst));
+  const unsigned ws = n / 64, bs = n % 64;
+  for (int i = 63; i >= 0; i--) {
+    const int s = i - (int)ws;
+    if (s < 0)
+      continue;
+    uint64_t v = src[s] << bs;
+    if (bs && s > 0)
+      v |= src[s - 1] >> (64 - bs);
+    dst[i] = v;
+  }
+  memcpy(x->w, dst, sizeof(dst));
+  x->nwords = 64;
+}
+
+extern "C" void gpqhe_mpi_release(MPI a)
+{
+  free(a);
+}
+
+extern "C" unsigned gpqhe_mpi_get_nbits(MPI a)
+{
+  for (int i = 63; i >= 0; i--)
+    if (a->w[i])
+      return (unsigned)(i * 64 + 64 - __builtin_clzll(a->w[i]));
+  return 0;
+}
+
+// ===========================================================================
+// Context
+// ===========================================================================
+static void set_seed_words(uint64_t seed)
+{
+  uint64_t z = seed;
+  for (int i = 0; i < 4; i++) {
+    z += 0x9E3779B97F4A7C15ull;
+    const uint64_t x = splitmix64_mix(z);
+    G.key.k[2 * i] = (uint32_t)x;
+    G.key.k[2 * i + 1] = (uint32_t)(x >> 32);
+  }
+  G.counter = 0;
+}
+
+extern "C" void gpqhe_set_seed(uint64_t seed)
+{
+  set_seed_words(seed);
+}
+
+static uint64_t default_seed()
+{
+  const char *e = getenv("GPQHE_SEED");
+  if (e && *e)
+    return strtoull(e, nullptr, 0);
+  uint64_t s = 0;
+  FILE *f = fopen("/dev/urandom", "rb");
+  if (!f || fread(&s, sizeof(s), 1, f) != 1)
+    gpqhe_die("cannot read /dev/urandom");
+  fclose(f);
+  return s;
+}
+
+extern "C" void hectx_init_params(const gpqhe_params_t *p)
+{
+  if (G.init)
+    hectx_exit();
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    gpqhe_die("no HIP device visible: libgpqhe.so runs on MI355X only (no CPU fallback)");
+  if (p->logn < 4 || p->logn > 17)
+    gpqhe_die("logn %u out of range [4, 17]", p->logn);
+  if (p->nlimbs < 1 || p->nspecial < 1 || p->nlimbs + p->nspecial > GPQHE_MAXMOD)
+    gpqhe_die("bad limb counts L=%u K=%u", p->nlimbs, p->nspecial);
+  if (p->q0_bits > 61 || p->qi_bits > 61 || p->p_bits > 61 || p->q0_bits < 32 || p->qi_bits < 32 ||
+      p->p_bits < 32)
+    gpqhe_die("prime sizes must be within [32, 61] bits");
+  Context &C = G;
+  C.logn = p->logn;
+  C.n = 1u << p->logn;
+  C.L = p->nlimbs;
+  C.K = p->nspecial;
+  C.nmod = C.L + C.K;
+  C.dnum = p->dnum ? p->dnum : p->nlimbs;
+  if (C.dnum > C.L)
+    C.dnum = C.L;
+  C.alpha = (C.L + C.dnum - 1) / C.dnum;
+  C.dnum = (C.L + C.alpha - 1) / C.alpha;
+  C.slots = p->slots ? p->slots : C.n / 2;
+  if ((C.slots & (C.slots - 1)) || C.slots > C.n / 2)
+    gpqhe_die("slots %u must be a power of two <= n/2", C.slots);
+  C.delta = p->delta;
+  const uint64_t two_n = 2ull * C.n;
+  unsigned used = 0;
+  C.q[used] = hm_pick_prime(p->q0_bits, two_n, C.q, used);
+  used++;
+  for (unsigned i = 1; i < C.L; i++, used++)
+    C.q[used] = hm_pick_prime(p->qi_bits, two_n, C.q, used);
+  for (unsigned i = 0; i < C.K; i++, used++)
+    C.q[used] = hm_pick_prime(p->p_bits, two_n, C.q, used);
+  for (unsigned m = 0; m < C.nmod; m++) {
+    hm_modconst(C.mc[m], C.q[m]);
+    C.psi[m] = hm_find_psi(C.q[m], C.n);
+    C.mc[m].ninv = hm_inv_mod(C.n, C.q[m]);
+    C.mc[m].ninvp = (uint64_t)(((unsigned __int128)C.mc[m].ninv << 64) / C.q[m]);
+    uint64_t pm = 1;
+    for (unsigned k = 0; k < C.K; k++)
+      pm = hm_mul_mod(pm, C.q[C.L + k] % C.q[m], C.q[m]);
+    C.mc[m].pmod = pm;
+    C.mc[m].pmodp = (uint64_t)(((unsigned __int128)pm << 64) / C.q[m]);
+  }
+  HIP_CHECK(hipGetDevice(&C.device));
+  (void)hipGetLastError();  // start from a clean error state
+  if (!C.own_stream)
+    HIP_CHECK(hipStreamCreateWithFlags(&C.own_stream, hipStreamNonBlocking));
+  if (!C.stream)
+    C.stream = C.own_stream;
+  tables_upload();
+  set_seed_words(p->seed ? p->seed : default_seed());
+  C.init = true;
+}
+
+static unsigned env_u(const char *name, unsigned dflt)
+{
+  const char *e = getenv(name);
+  return (e && *e) ? (unsigned)strtoul(e, nullptr, 0) : dflt;
+}
+
+extern "C" void hectx_init(unsigned int logn, MPI q, unsigned int slots, uint64_t Delta)
+{
+  gpqhe_params_t p;
+  memset(&p, 0, sizeof(p));
+  const unsigned logq = gpqhe_mpi_get_nbits(q) - 1;
+  const unsigned logd = 63 - (unsigned)__builtin_clzll(Delta);
+  p.logn = env_u("GPQHE_LOGN", logn);
+  p.slots = slots;
+  p.delta = (double)Delta;
+  p.qi_bits = logd;
+  p.nspecial = 1;
+  p.p_bits = 60;
+  unsigned L = env_u("GPQHE_NLIMBS", 0);
+  if (L) {
+    p.nlimbs = L;
+    p.q0_bits = 60;
+  } else {
+    L = 2;
+    while (logq > (L - 1) * logd + 61)
+      L++;
+    p.nlimbs = L;
+    p.q0_bits = logq - (L - 1) * logd;
+  }
+  p.dnum = env_u("GPQHE_DNUM", p.nlimbs);
+  p.seed = 0;
+  hectx_init_params(&p);
+}
+
+void gemv_cache_clear();
+
+extern "C" void hectx_exit(void)
+{
+  if (!G.init)
+    return;
+  HIP_CHECK(hipStreamSynchronize(G.stream));
+  gemv_cache_clear();
+  tables_free();
+  pool_release_all();
+  stage_release();
+  G.init = false;
+}
+
+extern "C" void hectx_info(gpqhe_info_t *info)
+{
+  check_ctx();
+  memset(info, 0, sizeof(*info));
+  info->logn = G.logn;
+  info->n = G.n;
+  info->nlimbs = G.L;
+  info->nspecial = G.K;
+  info->dnum = G.dnum;
+  info->alpha = G.alpha;
+  info->slots = G.slots;
+  info->delta = G.delta;
+  for (unsigned m = 0; m < G.nmod; m++) {
+    info->primes[m] = G.q[m];
+    info->psi[m] = G.psi[m];
+  }
+}
+
+extern "C" void gpqhe_set_stream(void *stream)
+{
+  if (G.stream)
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+  G.stream = stream ? (hipStream_t)stream : G.own_stream;
+}
+
+extern "C" void gpqhe_sync(void)
+{
+  if (G.stream)
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+}
+
+// ===========================================================================
+// Objects
+// ===========================================================================
+extern "C" void he_alloc_pk(he_pk_t *pk) { obj_alloc(pk, 2, G.L); }
+extern "C" void he_free_pk(he_pk_t *pk) { obj_free(pk); }
+extern "C" void he_alloc_sk(poly_mpi_t *sk) { obj_alloc(sk, 1, G.nmod); }
+extern "C" void he_free_sk(poly_mpi_t *sk) { obj_free(sk); }
+extern "C" void he_alloc_ct(he_ct_t *ct) { obj_alloc(ct, 2, G.L); }
+extern "C" void he_free_ct(he_ct_t *ct) { obj_free(ct); }
+extern "C" void he_alloc_pt(he_pt_t *pt) { obj_alloc(pt, 1, G.nmod); }
+extern "C" void he_free_pt(he_pt_t *pt) { obj_free(pt); }
+
+extern "C" void he_alloc_evk(he_evk_t *evk)
+{
+  check_ctx();
+  memset(evk, 0, sizeof(*evk));
+}
+
+extern "C" void he_free_evk(he_evk_t *evk) { obj_free(evk); }
+
+extern "C" size_t he_export(const void *vo, uint64_t *host)
+{
+  check_ctx();
+  const he_ct_t *o = OB(vo);
+  const size_t n = G.n;
+  HIP_CHECK(hipStreamSynchronize(G.stream));
+  size_t w = 0;
+  for (unsigned p = 0; p < o->npoly; p++) {
+    HIP_CHECK(hipMemcpy(host + w, limb(o, p, 0), (size_t)o->nlimbs * n * 8, hipMemcpyDeviceToHost));
+    w += (size_t)o->nlimbs * n;
+  }
+  return w;
+}
+
+extern "C" void he_import(void *vo, const uint64_t *host, unsigned int nlimbs, double scale, uint32_t flags)
+{
+  check_ctx();
+  he_ct_t *o = OB(vo);
+  if (!o->data) {
+    const uint32_t g = o->galois, dn = o->dnum;
+    if (!dn || dn != G.dnum)
+      gpqhe_die("he_import into an unallocated object (evk needs dnum=%u)", G.dnum);
+    obj_alloc(o, 2 * dn, G.nmod);
+    o->galois = g;
+    o->dnum = dn;
+  }
+  if (nlimbs > o->cap)
+    gpqhe_die("he_import: %u limbs > capacity %u", nlimbs, o->cap);
+  HIP_CHECK(hipStreamSynchronize(G.stream));
+  size_t w = 0;
+  for (unsigned p = 0; p < o->npoly; p++) {
+    HIP_CHECK(hipMemcpy(limb(o, p, 0), host + w, (size_t)nlimbs * G.n * 8, hipMemcpyHostToDevice));
+    w += (size_t)nlimbs * G.n;
+  }
+  o->nlimbs = nlimbs;
+  o->scale = scale;
+  o->flags = flags;
+}
+
+extern "C" void he_evk_meta(const he_evk_t *evk, uint32_t *galois, uint32_t *dnum)
+{
+  *galois = evk->galois;
+  *dnum = evk->dnum;
+}
+
+// ===========================================================================
+// Keys
+// ===========================================================================
+extern "C" void he_keypair(he_pk_t *pk, poly_mpi_t *sk)
+{
+  check_ctx();
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned m = 0; m < G.nmod; m++)
+    mods[m] = m;
+  sample_small_ntt(sk->data, mods, G.nmod, 0);  // s: ternary over all moduli
+  sk->nlimbs = G.nmod;
+  sample_uniform(limb(pk, 1, 0), mods, G.L);     // a
+  Ws e((size_t)G.L << G.logn);
+  sample_small_ntt(e.p, mods, G.L, 1);           // e
+  k_enc_sk_combine(limb(pk, 0, 0), limb(pk, 1, 0), e.p, sk->data, nullptr, G.L);  // -a s + e
+  pk->nlimbs = G.L;
+}
+
+static void gen_evk(he_evk_t *evk, const uint64_t *sprime, const poly_mpi_t *sk, uint32_t galois)
+{
+  if (evk->data)
+    obj_free(evk);
+  obj_alloc(evk, 2 * G.dnum, G.nmod);
+  evk->nlimbs = G.nmod;
+  evk->galois = galois;
+  evk->dnum = G.dnum;
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned m = 0; m < G.nmod; m++)
+    mods[m] = m;
+  Ws e((size_t)G.nmod << G.logn);
+  for (unsigned j = 0; j < G.dnum; j++) {
+    sample_uniform(limb(evk, 2 * j + 1, 0), mods, G.nmod);
+    sample_small_ntt(e.p, mods, G.nmod, 1);
+    const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, G.L);
+    k_evk_combine(limb(evk, 2 * j, 0), limb(evk, 2 * j + 1, 0), e.p, sk->data, sprime, lo, hi);
+  }
+}
+
+static uint64_t galois_of_rot(unsigned r)
+{
+  return hm_pow_mod(5, r, 2ull * G.n);
+}
+
+static void gen_rot_key(he_evk_t *evk, uint64_t g, const poly_mpi_t *sk)
+{
+  Ws sp((size_t)G.nmod << G.logn);
+  k_automorph(sp.p, sk->data, G.nmod, g);
+  gen_evk(evk, sp.p, sk, (uint32_t)g);
+}
+
+extern "C" void he_genrk(he_evk_t rk[], const poly_mpi_t *sk)
+{
+  check_ctx();
+  if (rk[0].data)
+    obj_free(&rk[0]);
+  rk[0].galois = 1;
+  for (unsigned r = 1; r < G.slots; r++)
+    gen_rot_key(&rk[r], galois_of_rot(r), sk);
+}
+
+extern "C" void he_genrot(he_evk_t *evk, unsigned int rot, const poly_mpi_t *sk)
+{
+  check_ctx();
+  gen_rot_key(evk, galois_of_rot(rot), sk);
+}
+
+extern "C" void he_genrlk(he_evk_t *rlk, const poly_mpi_t *sk)
+{
+  check_ctx();
+  Ws s2((size_t)G.nmod << G.logn);
+  k_square(s2.p, sk->data, G.nmod);
+  gen_evk(rlk, s2.p, sk, 1);
+}
+
+// ===========================================================================
+// Encoding / encryption
+// ===========================================================================
+// Encode z at `scale` into `dst` limbs for moduli mods[0..nm) (NTT domain).
+static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scale, const unsigned *mods,
+                         unsigned nm)
+{
+  std::vector<int64_t> coef(G.n);
+  hm_encode_coeffs(coef.data(), z, s, G.n, scale);
+  Ws dcoef(G.n);
+  upload(dcoef.p, coef.data(), (size_t)G.n * 8);
+  LimbSet ls = limbset(dst, mods, nm, 1, (size_t)nm << G.logn);
+  k_lift_i64(ls, (const int64_t *)dcoef.p);
+  k_ntt(ls, false);
+}
+
+extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int slots, double scale,
+                          unsigned int nlimbs)
+{
+  check_ctx();
+  if (nlimbs < 1 || nlimbs > G.L)
+    gpqhe_die("he_ecd_ex: bad level %u", nlimbs);
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned i = 0; i < nlimbs; i++)
+    mods[i] = i;
+  encode_limbs(pt->data, (const double *)z, slots, scale, mods, nlimbs);
+  pt->nlimbs = nlimbs;
+  pt->scale = scale;
+  pt->flags = 0;
+}
+
+extern "C" void he_ecd(he_pt_t *pt, const gpqhe_complex_t z[])
+{
+  he_ecd_ex(pt, z, G.slots, G.delta, G.L);
+}
+
+extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
+{
+  check_ctx();
+  const unsigned nl = pt->nlimbs;
+  const size_t words = (size_t)nl << G.logn;
+  Ws c(words);
+  HIP_CHECK(hipMemcpyAsync(c.p, pt->data, words * 8, hipMemcpyDeviceToDevice, G.stream));
+  if (!(pt->flags & GPQHE_F_COEFF))
+    k_ntt(qlimbs(c.p, nl, 1, words), true);
+  std::vector<uint64_t> host(words);
+  HIP_CHECK(hipMemcpyAsync(host.data(), c.p, words * 8, hipMemcpyDeviceToHost, G.stream));
+  HIP_CHECK(hipStreamSynchronize(G.stream));
+  hm_decode((double *)z, host.data(), nl, slots, G.n, pt->scale);
+}
+
+extern "C" void he_dcd(gpqhe_complex_t z[], const he_pt_t *pt)
+{
+  he_dcd_ex(z, pt, G.slots);
+}
+
+extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
+{
+  check_ctx();
+  const unsigned lvl = pt->nlimbs;
+  const size_t w = (size_t)lvl << G.logn;
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned i = 0; i < lvl; i++)
+    mods[i] = i;
+  Ws v(w), e0(w), e1(w);
+  sample_small_ntt(v.p, mods, lvl, 0);
+  sample_small_ntt(e0.p, mods, lvl, 1);
+  sample_small_ntt(e1.p, mods, lvl, 1);
+  k_enc_combine(limb(ct, 0, 0), limb(ct, 1, 0), v.p, e0.p, e1.p, limb(pk, 0, 0), limb(pk, 1, 0), pt->data, lvl);
+  ct->nlimbs = lvl;
+  ct->scale = pt->scale;
+  ct->flags = 0;
+}
+
+extern "C" void he_enc_sk(he_ct_t *ct, const he_pt_t *pt, const poly_mpi_t *sk)
+{
+  check_ctx();
+  const unsigned lvl = pt->nlimbs;
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned i = 0; i < lvl; i++)
+    mods[i] = i;
+  sample_uniform(limb(ct, 1, 0), mods, lvl);
+  Ws e((size_t)lvl << G.logn);
+  sample_small_ntt(e.p, mods, lvl, 1);
+  k_enc_sk_combine(limb(ct, 0, 0), limb(ct, 1, 0), e.p, sk->data, pt->data, lvl);
+  ct->nlimbs = lvl;
+  ct->scale = pt->scale;
+  ct->flags = 0;
+}
+
+extern "C" void he_dec(he_pt_t *pt, const he_ct_t *ct, const poly_mpi_t *sk)
+{
+  check_ctx();
+  k_dec(pt->data, limb(ct, 0, 0), limb(ct, 1, 0), sk->data, ct->nlimbs);
+  pt->nlimbs = ct->nlimbs;
+  pt->scale = ct->scale;
+  pt->flags = 0;
+}
+
+// ===========================================================================
+// Evaluation
+// ===========================================================================
+static void check_scales(double a, double b, const char *op)
+{
+  if (fabs(a / b - 1.0) > 1e-9)
+    gpqhe_die("%s: scale mismatch (%g vs %g)", op, a, b);
+}
+
+static void addsub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, int op)
+{
+  check_ctx();
+  check_scales(a->scale, b->scale, op ? "he_sub" : "he_add");
+  const unsigned lvl = std::min(a->nlimbs, b->nlimbs);
+  const double scale = a->scale;
+  k_binop(out->data, a->data, b->data, 2, lvl, pstride(out), pstride(a), pstride(b), op);
+  out->nlimbs = lvl;
+  out->scale = scale;
+  out->flags = 0;
+}
+
+extern "C" void he_add(he_ct_t *out, const he_ct_t *a, const he_ct_t *b) { addsub(out, a, b, 0); }
+extern "C" void he_sub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b) { addsub(out, a, b, 1); }
+
+extern "C" void he_neg(he_ct_t *ct)
+{
+  check_ctx();
+  k_neg(ct->data, 2, ct->nlimbs, pstride(ct));
+}
+
+extern "C" void he_copy_ct(he_ct_t *dst, const he_ct_t *src)
+{
+  check_ctx();
+  if (dst == src)
+    return;
+  const size_t bytes = ((size_t)src->nlimbs << G.logn) * 8;
+  for (unsigned p = 0; p < 2; p++)
+    HIP_CHECK(hipMemcpyAsync(limb(dst, p, 0), limb(src, p, 0), bytes, hipMemcpyDeviceToDevice, G.stream));
+  dst->nlimbs = src->nlimbs;
+  dst->scale = src->scale;
+  dst->flags = src->flags;
+}
+
+extern "C" void he_moddown(he_ct_t *ct)
+{
+  check_ctx();
+  if (ct->nlimbs < 2)
+    gpqhe_die("he_moddown: ciphertext at the lowest level");
+  ct->nlimbs--;
+}
+
+extern "C" void he_add_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt)
+{
+  check_ctx();
+  check_scales(a->scale, pt->scale, "he_add_pt");
+  const unsigned lvl = std::min(a->nlimbs, pt->nlimbs);
+  const double scale = a->scale;
+  if (out != a)
+    he_copy_ct(out, a);
+  k_add_pt(out->data, out->data, pt->data, lvl, pstride(out));
+  out->nlimbs = lvl;
+  out->scale = scale;
+  out->flags = 0;
+}
+
+extern "C" void he_mul_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt)
+{
+  check_ctx();
+  const unsigned lvl = std::min(a->nlimbs, pt->nlimbs);
+  const double scale = a->scale * pt->scale;
+  if (pstride(out) != pstride(a))
+    gpqhe_die("he_mul_pt: layout mismatch");
+  k_mul_pt(out->data, a->data, pt->data, lvl, pstride(a));
+  out->nlimbs = lvl;
+  out->scale = scale;
+  out->flags = 0;
+}
+
+// Tensor + relinearize [+ rescale] for `count` ciphertext pairs.
+//   a, b: ciphertext i at a + i*in_stride, c1 at + in_pstride;
+//   out:  polynomial p (= 2 i + {0,1}) at out + p*out_pstride.
+static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
+                      size_t in_pstride, unsigned count, unsigned lvl, const he_evk_t *rlk, bool rescale)
+{
+  if (!rlk->data || rlk->dnum != G.dnum)
+    gpqhe_die("relinearization key missing or built for another dnum");
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n;
+  const size_t d01_stride = 2 * lvl * n, d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n,
+               acc_stride = 2 * nm * n;
+  Ws d01(count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
+  k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
+  k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
+  k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  k_ntt(limbset(D.p, mods, nm, count * ndig, nm * n), false);
+  k_ks_inner(acc.p, D.p, count, D_stride, acc_stride, rlk->data, lvl, 1, d01.p, d01.p + lvl * n, d01_stride,
+             nullptr, false);
+  k_moddown(out, out_pstride, acc.p, nm * n, 2 * count, lvl, rescale ? 1 : 0);
+}
+
+static void mul_core(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk, bool rescale)
+{
+  check_ctx();
+  const unsigned lvl = std::min(a->nlimbs, b->nlimbs);
+  if (rescale && lvl < 2)
+    gpqhe_die("he_mul_rescale: no level left to rescale");
+  if (pstride(a) != pstride(b))
+    gpqhe_die("he_mul: layout mismatch");
+  const double scale = a->scale * b->scale;
+  mul_chunk(out->data, pstride(out), a->data, b->data, 0, pstride(a), 1, lvl, rlk, rescale);
+  out->nlimbs = rescale ? lvl - 1 : lvl;
+  out->scale = rescale ? scale / (double)G.q[lvl - 1] : scale;
+  out->flags = 0;
+}
+
+extern "C" void he_mul(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk)
+{
+  mul_core(out, a, b, rlk, false);
+}
+
+extern "C" void he_mul_rescale(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk)
+{
+  mul_core(out, a, b, rlk, true);
+}
+
+extern "C" void he_rescale(he_ct_t *ct)
+{
+  check_ctx();
+  const unsigned lvl = ct->nlimbs;
+  if (lvl < 2)
+    gpqhe_die("he_rescale: ciphertext at the lowest level");
+  k_moddown(ct->data, pstride(ct), ct->data, pstride(ct), 2, lvl, 2);
+  ct->scale /= (double)G.q[lvl - 1];
+  ct->nlimbs = lvl - 1;
+}
+
+static const he_evk_t *find_rot_key(const he_evk_t rk[], unsigned r, uint64_t g)
+{
+  const he_evk_t *k = &rk[r];
+  if (!k->data || k->galois != (uint32_t)g)
+    gpqhe_die("rotation key for r=%u (galois %llu) missing", r, (unsigned long long)g);
+  if (k->dnum != G.dnum)
+    gpqhe_die("rotation key built for dnum=%u, context dnum=%u", k->dnum, G.dnum);
+  return k;
+}
+
+// c1 of x -> coefficient domain -> ModUp digits (NTT domain) in D.
+static void hoist_modup(uint64_t *D, const he_ct_t *x, unsigned lvl)
+{
+  const size_t n = G.n;
+  Ws c1c((size_t)lvl * n);
+  HIP_CHECK(hipMemcpyAsync(c1c.p, limb(x, 1, 0), (size_t)lvl * n * 8, hipMemcpyDeviceToDevice, G.stream));
+  k_ntt(qlimbs(c1c.p, lvl, 1, lvl * n), true);
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  k_modup(D, c1c.p, 1, lvl * n, (size_t)ndig * nm * n, lvl);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  k_ntt(limbset(D, mods, nm, ndig, nm * n), false);
+}
+
+extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const he_evk_t rk[])
+{
+  check_ctx();
+  rot %= G.slots;
+  if (!rot) {
+    he_copy_ct(out, in);
+    return;
+  }
+  const unsigned lvl = in->nlimbs, nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n;
+  const uint64_t g = galois_of_rot(rot);
+  const he_evk_t *k = find_rot_key(rk, rot, g);
+  Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
+  hoist_modup(D.p, in, lvl);
+  k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(in, 0, 0), nullptr, 0, nullptr, false);
+  const double scale = in->scale;
+  k_moddown(out->data, pstride(out), acc.p, nm * n, 2, lvl, 0);
+  out->nlimbs = lvl;
+  out->scale = scale;
+  out->flags = 0;
+}
+
+// ---------------------------------------------------------------------------
+// he_gemv: diagonal method, hoisted ModUp, diagonals encoded at scale q_top
+// over the QP basis, one ModDown-and-rescale by P q_top at the end.
+// Encoded diagonals are cached by content (the caller recomputes the same
+// gain matrices every control step: reference src/hempc.c:232-238).
+// ---------------------------------------------------------------------------
+static std::unordered_map<std::string, uint64_t *> g_gemv_cache;
+static size_t g_gemv_cache_bytes = 0;
+
+void gemv_cache_clear()
+{
+  for (auto &kv : g_gemv_cache)
+    pool_free(kv.second);
+  g_gemv_cache.clear();
+  g_gemv_cache_bytes = 0;
+}
+
+static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
+{
+  std::string key((const char *)diag, (size_t)s * 16);
+  key.append((const char *)&lvl, sizeof(lvl));
+  auto it = g_gemv_cache.find(key);
+  if (it != g_gemv_cache.end())
+    return it->second;
+  unsigned mods[GPQHE_MAXMOD];
+  const unsigned nm = basis_qp(lvl, mods);
+  const size_t bytes = ((size_t)nm << G.logn) * 8;
+  if (g_gemv_cache_bytes + bytes > ((size_t)1 << 31))
+    gemv_cache_clear();
+  uint64_t *p = (uint64_t *)pool_alloc(bytes);
+  encode_limbs(p, diag, s, (double)G.q[lvl - 1], mods, nm);
+  g_gemv_cache[key] = p;
+  g_gemv_cache_bytes += bytes;
+  return p;
+}
+
+extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
+{
+  check_ctx();
+  const unsigned lvl = x->nlimbs, s = G.slots;
+  if (lvl < 2)
+    gpqhe_die("he_gemv: input at the lowest level");
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n;
+  const double *Md = (const double *)M;
+  Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
+  hoist_modup(D.p, x, lvl);
+  HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
+  std::vector<double> diag(2 * (size_t)s);
+  for (unsigned d = 0; d < s; d++) {
+    bool nz = false;
+    for (unsigned i = 0; i < s; i++) {
+      const size_t src = (size_t)i * s + (i + d) % s;
+      diag[2 * i] = Md[2 * src];
+      diag[2 * i + 1] = Md[2 * src + 1];
+      nz |= diag[2 * i] != 0.0 || diag[2 * i + 1] != 0.0;
+    }
+    if (!nz)
+      continue;
+    const uint64_t *pt = diag_pt(diag.data(), s, lvl);
+    if (d == 0) {
+      k_ks_inner(acc.p, D.p, 1, 0, 0, nullptr, lvl, 1, limb(x, 0, 0), limb(x, 1, 0), 0, pt, true);
+      continue;
+    }
+    const uint64_t g = galois_of_rot(d);
+    const he_evk_t *k = find_rot_key(rk, d, g);
+    k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(x, 0, 0), nullptr, 0, pt, true);
+  }
+  const double scale = x->scale;
+  k_moddown(y->data, pstride(y), acc.p, nm * n, 2, lvl, 1);
+  y->nlimbs = lvl - 1;
+  y->scale = scale;
+  y->flags = 0;
+}
+
+// ===========================================================================
+// Batched entry points
+// ===========================================================================
+extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uint64_t *b, size_t count,
+                                     unsigned int nlimbs, const he_evk_t *rlk)
+{
+  check_ctx();
+  const unsigned lvl = nlimbs;
+  if (lvl < 2 || lvl > G.L)
+    gpqhe_die("he_mul_rescale_batch: bad level %u", lvl);
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n;
+  const size_t per_ct = (size_t)(2 * lvl + lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
+  const size_t budget = (size_t)2 << 30;
+  size_t chunk = std::max<size_t>(1, budget / per_ct);
+  chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));
+  const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
+  for (size_t c0 = 0; c0 < count; c0 += chunk) {
+    const unsigned cnt = (unsigned)std::min(chunk, count - c0);
+    mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n,
+              cnt, lvl, rlk, true);
+  }
+}
+
+static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)
+{
+  check_ctx();
+  const size_t per = 65535 / nlimbs;
+  for (size_t p0 = 0; p0 < npolys; p0 += per) {
+    const unsigned cnt = (unsigned)std::min(per, npolys - p0);
+    k_ntt(qlimbs(data + p0 * nlimbs * G.n, nlimbs, cnt, (size_t)nlimbs * G.n), inverse);
+  }
+}
+
+extern "C" void poly_ntt_batch(uint64_t *data, size_t npolys, unsigned int nlimbs)
+{
+  ntt_batch(data, npolys, nlimbs, false);
+}
+
+extern "C" void poly_intt_batch(uint64_t *data, size_t npolys, unsigned int nlimbs)
+{
+  ntt_batch(data, npolys, nlimbs, true);
+}
+
+extern "C" void poly_fill_uniform(uint64_t *data, size_t npolys, unsigned int nlimbs, uint64_t seed)
+{
+  check_ctx();
+  k_fill_uniform(data, npolys, nlimbs, seed);
+}

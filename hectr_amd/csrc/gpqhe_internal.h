@@ -1,0 +1,253 @@
+// gpqhe_internal.h - shared definitions of the MI355X CKKS engine
+// (libgpqhe.so): modular arithmetic, RNG, device tables, host context.
+//
+// Arithmetic contract: every residue stored in HBM is canonical in [0, q).
+// Primes are < 2^61, so 64-bit lanes hold [0, 4q) lazily where a kernel
+// wants it.  The algorithms (prime/root choice, NTT ordering, basis
+// conversion, RNG streams, encode rounding) are the ones the CPU oracle
+// (oracle/ckks_oracle.c) defines, so outputs are bit-identical to it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <vector>
+
+#include "../../include/gpqhe.h"
+
+#define GPQHE_MAXMOD 64
+
+#define HIP_CHECK(expr)                                                        \
+  do {                                                                         \
+    hipError_t err_ = (expr);                                                  \
+    if (err_ != hipSuccess)                                                    \
+      gpqhe_die("HIP error %s at %s:%d: %s", hipGetErrorName(err_), __FILE__, \
+                __LINE__, hipGetErrorString(err_));                            \
+  } while (0)
+
+[[noreturn]] void gpqhe_die(const char *fmt, ...);
+
+// ---------------------------------------------------------------------------
+// Per-modulus constants (device copy in ModTab array).
+// ---------------------------------------------------------------------------
+struct ModConst {
+  uint64_t q;
+  uint64_t mu;     // floor(2^(2k) / q), Barrett
+  uint32_t k;      // bit length of q
+  uint32_t pad;
+  uint64_t ninv, ninvp;  // n^-1 and Shoup companion
+  uint64_t pmod, pmodp;  // [P]_q (product of the special primes) + Shoup
+};
+
+// ---------------------------------------------------------------------------
+// Modular arithmetic (host + device).
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+__host__ __device__ __forceinline__ uint64_t add_mod(uint64_t a, uint64_t b, uint64_t q)
+{
+  uint64_t r = a + b;
+  return r >= q ? r - q : r;
+}
+
+__host__ __device__ __forceinline__ uint64_t sub_mod(uint64_t a, uint64_t b, uint64_t q)
+{
+  return a >= b ? a - b : a + q - b;
+}
+
+__host__ __device__ __forceinline__ uint64_t neg_mod(uint64_t a, uint64_t q)
+{
+  return a ? q - a : 0;
+}
+
+// Barrett product of a, b < q (k = bitlen(q) <= 61).
+__host__ __device__ __forceinline__ uint64_t mul_mod(uint64_t a, uint64_t b, const ModConst &m)
+{
+  const uint64_t lo = a * b, hi = mulhi64(a, b);
+  const uint64_t t = (hi << (65 - m.k)) | (lo >> (m.k - 1));
+  const uint64_t plo = t * m.mu, phi = mulhi64(t, m.mu);
+  const uint64_t est = (phi << (63 - m.k)) | (plo >> (m.k + 1));
+  uint64_t r = lo - est * m.q;
+  r = r >= m.q ? r - m.q : r;
+  return r >= m.q ? r - m.q : r;
+}
+
+// Shoup product: w < q constant with wp = floor(w 2^64 / q); a < 2^64.
+__host__ __device__ __forceinline__ uint64_t mul_shoup(uint64_t a, uint64_t w, uint64_t wp, uint64_t q)
+{
+  const uint64_t qh = mulhi64(a, wp);
+  const uint64_t r = a * w - qh * q;
+  return r >= q ? r - q : r;
+}
+
+// Shoup without the final correction: result in [0, 2q).
+__host__ __device__ __forceinline__ uint64_t mul_shoup_lazy(uint64_t a, uint64_t w, uint64_t wp, uint64_t q)
+{
+  return a * w - mulhi64(a, wp) * q;
+}
+
+// x mod q for arbitrary 64-bit x (q < 2^61): reduce via Barrett on (0:x).
+__host__ __device__ __forceinline__ uint64_t reduce64(uint64_t x, const ModConst &m)
+{
+  const uint64_t t = x >> (m.k - 1);
+  const uint64_t plo = t * m.mu, phi = mulhi64(t, m.mu);
+  const uint64_t est = (phi << (63 - m.k)) | (plo >> (m.k + 1));
+  uint64_t r = x - est * m.q;
+  r = r >= m.q ? r - m.q : r;
+  return r >= m.q ? r - m.q : r;
+}
+
+// ---------------------------------------------------------------------------
+// ChaCha20 block (state: constants | key | counter | 0 | stream lo | hi).
+// ---------------------------------------------------------------------------
+struct ChachaKey {
+  uint32_t k[8];
+};
+
+#define GPQHE_ROTL32(v, c) (((v) << (c)) | ((v) >> (32 - (c))))
+#define GPQHE_QR(a, b, c, d)                                                   \
+  a += b; d ^= a; d = GPQHE_ROTL32(d, 16);                                     \
+  c += d; b ^= c; b = GPQHE_ROTL32(b, 12);                                     \
+  a += b; d ^= a; d = GPQHE_ROTL32(d, 8);                                      \
+  c += d; b ^= c; b = GPQHE_ROTL32(b, 7)
+
+__host__ __device__ __forceinline__ void chacha20_block(uint32_t out[16], const ChachaKey &key,
+                                                        uint64_t stream, uint32_t counter)
+{
+  uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                    key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
+                    counter, 0u, (uint32_t)stream, (uint32_t)(stream >> 32)};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    x[i] = s[i];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    GPQHE_QR(x[0], x[4], x[8], x[12]);
+    GPQHE_QR(x[1], x[5], x[9], x[13]);
+    GPQHE_QR(x[2], x[6], x[10], x[14]);
+    GPQHE_QR(x[3], x[7], x[11], x[15]);
+    GPQHE_QR(x[0], x[5], x[10], x[15]);
+    GPQHE_QR(x[1], x[6], x[11], x[12]);
+    GPQHE_QR(x[2], x[7], x[8], x[13]);
+    GPQHE_QR(x[3], x[4], x[9], x[14]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++)
+    out[i] = x[i] + s[i];
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64_mix(uint64_t z)
+{
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// Limb sets: `count` limbs, limb v at base + (v / per) * stride + (v % per) * n,
+// reduced modulo mods[v % per].  Passed by value to kernels.
+// ---------------------------------------------------------------------------
+struct LimbSet {
+  uint64_t *base;
+  size_t stride;      // words between groups of `per` limbs
+  uint32_t per;
+  uint32_t count;
+  uint8_t mods[GPQHE_MAXMOD];
+
+  __host__ __device__ __forceinline__ uint64_t *limb(uint32_t v, uint32_t logn) const
+  {
+    return base + (size_t)(v / per) * stride + ((size_t)(v % per) << logn);
+  }
+  __host__ __device__ __forceinline__ uint32_t mod(uint32_t v) const { return mods[v % per]; }
+};
+
+// ---------------------------------------------------------------------------
+// Host context (process-global singleton).
+// ---------------------------------------------------------------------------
+struct DevTables {
+  ModConst *mc;        // [nmod]
+  uint64_t *tw, *twp;  // [nmod][n] psi^brev(k) (+ Shoup)
+  uint64_t *itw, *itwp;
+};
+
+struct Context {
+  bool init = false;
+  unsigned logn = 0, n = 0, L = 0, K = 0, nmod = 0, dnum = 0, alpha = 0, slots = 0;
+  double delta = 0;
+  uint64_t q[GPQHE_MAXMOD];
+  uint64_t psi[GPQHE_MAXMOD];
+  ModConst mc[GPQHE_MAXMOD];
+  ChachaKey key;
+  uint64_t counter = 0;
+  DevTables dev{};
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  int device = 0;
+};
+
+extern Context G;
+
+// ---------------------------------------------------------------------------
+// Host helpers (host_math.cpp)
+// ---------------------------------------------------------------------------
+uint64_t hm_pow_mod(uint64_t b, uint64_t e, uint64_t q);
+uint64_t hm_inv_mod(uint64_t a, uint64_t q);
+void hm_modconst(ModConst &m, uint64_t q);
+uint64_t hm_mul_mod(uint64_t a, uint64_t b, uint64_t q);
+uint64_t hm_pick_prime(unsigned bits, uint64_t two_n, const uint64_t *used, unsigned nused);
+uint64_t hm_find_psi(uint64_t q, uint64_t n);
+unsigned hm_brev(unsigned x, unsigned bits);
+void hm_encode_coeffs(int64_t *coef, const double *z_interleaved, unsigned s, unsigned n, double scale);
+void hm_decode(double *z_interleaved, const uint64_t *coef_limbs, unsigned nl, unsigned s, unsigned n,
+               double scale);
+
+// ---------------------------------------------------------------------------
+// Device memory pool (stream-ordered reuse on the engine stream).
+// ---------------------------------------------------------------------------
+void *pool_alloc(size_t bytes);
+void pool_free(void *p);
+void pool_release_all();
+
+// ---------------------------------------------------------------------------
+// Kernel launchers (kernels.hip)
+// ---------------------------------------------------------------------------
+void k_ntt(const LimbSet &s, bool inverse);
+void k_binop(uint64_t *out, const uint64_t *a, const uint64_t *b, unsigned npoly, unsigned lvl,
+             size_t out_pstride, size_t a_pstride, size_t b_pstride, int op);
+void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t pstride);
+// d01 [count][2][lvl][n] (stride d_stride) <- (a0 b0, a0 b1 + a1 b0); d2 [count][lvl][n] <- a1 b1
+void k_tensor(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b, unsigned lvl,
+              size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride);
+void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned lvl);
+void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
+void k_sample_uniform(const LimbSet &dst, uint64_t stream);
+void k_lift_i64(const LimbSet &dst, const int64_t *coef);
+void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
+                   const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl);
+void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,
+                      unsigned lvl);
+void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *sprime,
+                   unsigned lo, unsigned hi);
+void k_automorph(uint64_t *out, const uint64_t *in, unsigned nlimbs, uint64_t g);
+void k_square(uint64_t *out, const uint64_t *in, unsigned nlimbs);
+void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl);
+// acc [count][2][lvl+K][n] (stride acc_stride): acc0 then acc1
+void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_stride, size_t acc_stride,
+                const uint64_t *evk, unsigned lvl, uint64_t g, const uint64_t *c0, const uint64_t *c1,
+                size_t c_stride, const uint64_t *pt, bool accumulate);
+// mode 0: divide by P; 1: by P q_{lvl-1}; 2: by q_{lvl-1} (X over q limbs only)
+void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned nx_poly,
+               unsigned lvl, int mode);
+void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t seed);
+void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
+void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
+void tables_upload();
+void tables_free();

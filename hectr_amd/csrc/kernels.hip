@@ -1,0 +1,1046 @@
+// kernels.hip - gfx950 kernels of the CKKS engine.
+//
+// NTT: negacyclic, psi merged into the twiddles, forward Cooley-Tukey
+// (natural -> bit-reversed), inverse Gentleman-Sande (bit-reversed ->
+// natural), the ordering of oracle/ckks_oracle.c:ntt_limb/intt_limb.  For a
+// butterfly on local element j at distance t the twiddle is
+//     tw[(base + j) >> (log2 t + 1)]
+// with base = n for a whole-limb tile, n1 for a column tile of the n1 x n2
+// decomposition and (n1 + row) * n2 for a row tile.  One workgroup owns one
+// LDS tile; each round keeps 2^R elements per thread in registers for R
+// radix-2 stages (R <= 4), so a 256-point sub-transform costs two LDS round
+// trips.
+//
+// All other kernels are elementwise over (limb, coefficient) and stream HBM
+// with one 8-byte word per lane, canonical residues in and out.
+#include "gpqhe_internal.h"
+
+#include <map>
+#include <tuple>
+
+#define TPB 256
+
+static inline dim3 grid1(size_t n, unsigned tpb = TPB)
+{
+  return dim3((unsigned)((n + tpb - 1) / tpb));
+}
+
+__device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
+{
+  return __brev(x) >> (32 - bits);
+}
+
+// ===========================================================================
+// NTT rounds on an LDS tile.
+// Tile: nsub sub-transforms of T = 2^logT points; element (sub, j) at
+// lds[sub * SS + j * ES].  base(sub) = base0 + sub * bstep.
+// ===========================================================================
+// In one round a group holds elements b + k*tlo (k < E).  Stage s of the
+// round uses the 2^s (forward) or 2^(R-1-s) (inverse) twiddles
+//   tw[Bs + u],  Bs = (base + b_high) >> (log2 t + 1 + log2(u-range)),
+// i.e. contiguous runs, so a radix-16 group loads exactly 15 twiddle pairs.
+template <int LOGE, bool SUB_MAJOR>
+__device__ __forceinline__ void fwd_round(uint64_t *lds, int nsub, int logT, int log_thi, int SS, int ES,
+                                          uint64_t base0, uint64_t bstep, const uint64_t *__restrict__ tw,
+                                          const uint64_t *__restrict__ twp, uint64_t q)
+{
+  constexpr int E = 1 << LOGE;
+  const int log_tlo = log_thi - LOGE + 1;
+  const int tlo = 1 << log_tlo;
+  const int gps = (1 << logT) >> LOGE;  // groups per sub
+  const int total = nsub * gps;
+  for (int g = threadIdx.x; g < total; g += blockDim.x) {
+    int sub, grp;
+    if (SUB_MAJOR) {
+      sub = g / gps;
+      grp = g - sub * gps;
+    } else {
+      sub = g % nsub;
+      grp = g / nsub;
+    }
+    const int bhi = (grp >> log_tlo) << (log_thi + 1);
+    const int b = bhi | (grp & (tlo - 1));
+    const uint64_t bb = base0 + (uint64_t)sub * bstep + (uint64_t)bhi;
+    uint64_t W[E - 1], WP[E - 1];
+#pragma unroll
+    for (int s = 0; s < LOGE; s++) {
+      const uint64_t Bs = bb >> (log_thi - s + 1);
+#pragma unroll
+      for (int u = 0; u < (1 << s); u++) {
+        W[(1 << s) - 1 + u] = tw[Bs + u];
+        WP[(1 << s) - 1 + u] = twp[Bs + u];
+      }
+    }
+    uint64_t x[E];
+#pragma unroll
+    for (int k = 0; k < E; k++)
+      x[k] = lds[sub * SS + (b + k * tlo) * ES];
+#pragma unroll
+    for (int s = 0; s < LOGE; s++) {
+      const int half = E >> (s + 1);
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if (k & half)
+          continue;
+        const int wi = (1 << s) - 1 + (k >> (LOGE - s));
+        const uint64_t U = x[k];
+        const uint64_t V = mul_shoup(x[k + half], W[wi], WP[wi], q);
+        x[k] = add_mod(U, V, q);
+        x[k + half] = sub_mod(U, V, q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < E; k++)
+      lds[sub * SS + (b + k * tlo) * ES] = x[k];
+  }
+}
+
+template <int LOGE, bool SUB_MAJOR>
+__device__ __forceinline__ void inv_round(uint64_t *lds, int nsub, int logT, int log_tlo, int SS, int ES,
+                                          uint64_t base0, uint64_t bstep, const uint64_t *__restrict__ tw,
+                                          const uint64_t *__restrict__ twp, uint64_t q)
+{
+  constexpr int E = 1 << LOGE;
+  const int log_thi = log_tlo + LOGE - 1;
+  const int tlo = 1 << log_tlo;
+  const int gps = (1 << logT) >> LOGE;
+  const int total = nsub * gps;
+  for (int g = threadIdx.x; g < total; g += blockDim.x) {
+    int sub, grp;
+    if (SUB_MAJOR) {
+      sub = g / gps;
+      grp = g - sub * gps;
+    } else {
+      sub = g % nsub;
+      grp = g / nsub;
+    }
+    const int bhi = (grp >> log_tlo) << (log_thi + 1);
+    const int b = bhi | (grp & (tlo - 1));
+    const uint64_t bb = base0 + (uint64_t)sub * bstep + (uint64_t)bhi;
+    // stage s uses 2^(LOGE-1-s) twiddles; slot offset = E - 2^(LOGE-s)
+    uint64_t W[E - 1], WP[E - 1];
+#pragma unroll
+    for (int s = 0; s < LOGE; s++) {
+      const uint64_t Bs = bb >> (log_tlo + s + 1);
+#pragma unroll
+      for (int u = 0; u < (1 << (LOGE - 1 - s)); u++) {
+        W[E - (1 << (LOGE - s)) + u] = tw[Bs + u];
+        WP[E - (1 << (LOGE - s)) + u] = twp[Bs + u];
+      }
+    }
+    uint64_t x[E];
+#pragma unroll
+    for (int k = 0; k < E; k++)
+      x[k] = lds[sub * SS + (b + k * tlo) * ES];
+#pragma unroll
+    for (int s = 0; s < LOGE; s++) {
+      const int half = 1 << s;
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if (k & half)
+          continue;
+        const int wi = E - (1 << (LOGE - s)) + (k >> (s + 1));
+        const uint64_t U = x[k], V = x[k + half];
+        x[k] = add_mod(U, V, q);
+        x[k + half] = mul_shoup(sub_mod(U, V, q), W[wi], WP[wi], q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < E; k++)
+      lds[sub * SS + (b + k * tlo) * ES] = x[k];
+  }
+}
+
+// Forward: rounds from the largest distance down; first round takes the
+// remainder so later rounds are full radix-16.
+template <bool SUB_MAJOR>
+__device__ __forceinline__ void tile_fwd(uint64_t *lds, int nsub, int logT, int SS, int ES, uint64_t base0, uint64_t bstep,
+                         const uint64_t *tw, const uint64_t *twp, uint64_t q)
+{
+  int remaining = logT;
+  int log_thi = logT - 1;
+  int first = logT % 4 ? logT % 4 : 4;
+  while (remaining > 0) {
+    const int r = first;
+    switch (r) {
+    case 1: fwd_round<1, SUB_MAJOR>(lds, nsub, logT, log_thi, SS, ES, base0, bstep, tw, twp, q); break;
+    case 2: fwd_round<2, SUB_MAJOR>(lds, nsub, logT, log_thi, SS, ES, base0, bstep, tw, twp, q); break;
+    case 3: fwd_round<3, SUB_MAJOR>(lds, nsub, logT, log_thi, SS, ES, base0, bstep, tw, twp, q); break;
+    default: fwd_round<4, SUB_MAJOR>(lds, nsub, logT, log_thi, SS, ES, base0, bstep, tw, twp, q); break;
+    }
+    __syncthreads();
+    remaining -= r;
+    log_thi -= r;
+    first = 4;
+  }
+}
+
+template <bool SUB_MAJOR>
+__device__ __forceinline__ void tile_inv(uint64_t *lds, int nsub, int logT, int SS, int ES, uint64_t base0, uint64_t bstep,
+                         const uint64_t *tw, const uint64_t *twp, uint64_t q)
+{
+  int log_tlo = 0;
+  int remaining = logT;
+  while (remaining > 0) {
+    const int r = remaining >= 4 ? 4 : remaining;
+    switch (r) {
+    case 1: inv_round<1, SUB_MAJOR>(lds, nsub, logT, log_tlo, SS, ES, base0, bstep, tw, twp, q); break;
+    case 2: inv_round<2, SUB_MAJOR>(lds, nsub, logT, log_tlo, SS, ES, base0, bstep, tw, twp, q); break;
+    case 3: inv_round<3, SUB_MAJOR>(lds, nsub, logT, log_tlo, SS, ES, base0, bstep, tw, twp, q); break;
+    default: inv_round<4, SUB_MAJOR>(lds, nsub, logT, log_tlo, SS, ES, base0, bstep, tw, twp, q); break;
+    }
+    __syncthreads();
+    remaining -= r;
+    log_tlo += r;
+  }
+}
+
+// Whole limb in one LDS tile (n <= 4096: 32 KiB).  grid.y = limb.
+template <bool inverse>
+__global__ void __launch_bounds__(TPB) ntt_whole_kernel(LimbSet s, unsigned logn, DevTables t)
+{
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const unsigned n = 1u << logn;
+  const unsigned v = blockIdx.y;
+  uint64_t *x = s.limb(v, logn);
+  const unsigned m = s.mod(v);
+  const ModConst mc = t.mc[m];
+  for (unsigned i = threadIdx.x; i < n; i += blockDim.x)
+    lds[i] = x[i];
+  __syncthreads();
+  if constexpr (!inverse) {
+    tile_fwd<true>(lds, 1, logn, 0, 1, n, 0, t.tw + ((size_t)m << logn), t.twp + ((size_t)m << logn), mc.q);
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x)
+      x[i] = lds[i];
+  } else {
+    tile_inv<true>(lds, 1, logn, 0, 1, n, 0, t.itw + ((size_t)m << logn), t.itwp + ((size_t)m << logn), mc.q);
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x)
+      x[i] = mul_shoup(lds[i], mc.ninv, mc.ninvp, mc.q);
+  }
+}
+
+// Column pass of n = n1 x n2: tile = n1 rows x COLS columns.
+// grid.x = n2 / COLS, grid.y = limb.
+#define COLS 16
+template <bool inverse>
+__global__ void __launch_bounds__(TPB) ntt_cols_kernel(LimbSet s, unsigned logn, unsigned logn1, DevTables t)
+{
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const unsigned logn2 = logn - logn1;
+  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
+  const unsigned v = blockIdx.y;
+  uint64_t *x = s.limb(v, logn);
+  const unsigned m = s.mod(v);
+  const ModConst mc = t.mc[m];
+  const unsigned col0 = blockIdx.x * COLS;
+  constexpr int ES = COLS + 1;
+  for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
+    const unsigned r = e / COLS, c = e % COLS;
+    lds[r * ES + c] = x[(size_t)r * n2 + col0 + c];
+  }
+  __syncthreads();
+  if constexpr (!inverse) {
+    tile_fwd<false>(lds, COLS, logn1, 1, ES, n1, 0, t.tw + ((size_t)m << logn), t.twp + ((size_t)m << logn),
+                    mc.q);
+    for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
+      const unsigned r = e / COLS, c = e % COLS;
+      x[(size_t)r * n2 + col0 + c] = lds[r * ES + c];
+    }
+  } else {
+    tile_inv<false>(lds, COLS, logn1, 1, ES, n1, 0, t.itw + ((size_t)m << logn), t.itwp + ((size_t)m << logn),
+                    mc.q);
+    for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
+      const unsigned r = e / COLS, c = e % COLS;
+      x[(size_t)r * n2 + col0 + c] = mul_shoup(lds[r * ES + c], mc.ninv, mc.ninvp, mc.q);
+    }
+  }
+}
+
+// Row pass: tile = ROWS rows x n2 columns; grid.x = n1 / ROWS.
+template <bool inverse>
+__global__ void __launch_bounds__(TPB) ntt_rows_kernel(LimbSet s, unsigned logn, unsigned logn1, unsigned rows,
+                                                        DevTables t)
+{
+  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+  const unsigned logn2 = logn - logn1;
+  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
+  const unsigned v = blockIdx.y;
+  uint64_t *x = s.limb(v, logn);
+  const unsigned m = s.mod(v);
+  const ModConst mc = t.mc[m];
+  const unsigned row0 = blockIdx.x * rows;
+  const int SS = n2 + 1;
+  uint64_t *xt = x + (size_t)row0 * n2;
+  for (unsigned e = threadIdx.x; e < rows * n2; e += blockDim.x) {
+    const unsigned r = e >> logn2, c = e & (n2 - 1);
+    lds[r * SS + c] = xt[e];
+  }
+  __syncthreads();
+  const uint64_t base0 = ((uint64_t)n1 + row0) << logn2;
+  if constexpr (!inverse)
+    tile_fwd<true>(lds, rows, logn2, SS, 1, base0, n2, t.tw + ((size_t)m << logn), t.twp + ((size_t)m << logn),
+                   mc.q);
+  else
+    tile_inv<true>(lds, rows, logn2, SS, 1, base0, n2, t.itw + ((size_t)m << logn),
+                   t.itwp + ((size_t)m << logn), mc.q);
+  for (unsigned e = threadIdx.x; e < rows * n2; e += blockDim.x) {
+    const unsigned r = e >> logn2, c = e & (n2 - 1);
+    xt[e] = lds[r * SS + c];
+  }
+}
+
+void k_ntt(const LimbSet &s, bool inverse)
+{
+  if (!s.count)
+    return;
+  const unsigned logn = G.logn, n = G.n;
+  if (s.count > 65535)
+    gpqhe_die("k_ntt: %u limbs in one launch", s.count);
+  if (logn <= 12) {
+    if (inverse)
+      hipLaunchKernelGGL(ntt_whole_kernel<true>, dim3(1, s.count), dim3(TPB), n * 8, G.stream, s, logn, G.dev);
+    else
+      hipLaunchKernelGGL(ntt_whole_kernel<false>, dim3(1, s.count), dim3(TPB), n * 8, G.stream, s, logn, G.dev);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const unsigned logn1 = logn / 2;  // 13:6x7 14:7x7 15:7x8 16:8x8 17:8x9
+  const unsigned logn2 = logn - logn1;
+  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
+  const unsigned rows = n2 >= 512 ? 8 : 16;
+  const size_t lds_cols = (size_t)n1 * (COLS + 1) * 8, lds_rows = (size_t)rows * (n2 + 1) * 8;
+  if (!inverse) {
+    hipLaunchKernelGGL(ntt_cols_kernel<false>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s, logn,
+                       logn1, G.dev);
+    hipLaunchKernelGGL(ntt_rows_kernel<false>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
+                       logn1, rows, G.dev);
+  } else {
+    hipLaunchKernelGGL(ntt_rows_kernel<true>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
+                       logn1, rows, G.dev);
+    hipLaunchKernelGGL(ntt_cols_kernel<true>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s, logn,
+                       logn1, G.dev);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+// ===========================================================================
+// Elementwise kernels
+// ===========================================================================
+// out = a op b over npoly x lvl limbs; op 0 add, 1 sub.
+__global__ void binop_kernel(uint64_t *out, const uint64_t *a, const uint64_t *b, unsigned logn, unsigned lvl,
+                             size_t os, size_t as, size_t bs, int op, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned limb = blockIdx.y, p = blockIdx.z;
+  if (i >= n)
+    return;
+  const uint64_t q = mc[limb].q;
+  const uint64_t x = a[p * as + ((size_t)limb << logn) + i], y = b[p * bs + ((size_t)limb << logn) + i];
+  out[p * os + ((size_t)limb << logn) + i] = op ? sub_mod(x, y, q) : add_mod(x, y, q);
+}
+
+void k_binop(uint64_t *out, const uint64_t *a, const uint64_t *b, unsigned npoly, unsigned lvl, size_t os,
+             size_t as, size_t bs, int op)
+{
+  hipLaunchKernelGGL(binop_kernel, dim3((G.n + TPB - 1) / TPB, lvl, npoly), dim3(TPB), 0, G.stream, out, a, b,
+                     G.logn, lvl, os, as, bs, op, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void neg_kernel(uint64_t *x, unsigned logn, size_t ps, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  uint64_t *p = x + blockIdx.z * ps + ((size_t)blockIdx.y << logn) + i;
+  *p = neg_mod(*p, mc[blockIdx.y].q);
+}
+
+void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t ps)
+{
+  hipLaunchKernelGGL(neg_kernel, dim3((G.n + TPB - 1) / TPB, lvl, npoly), dim3(TPB), 0, G.stream, x, G.logn, ps,
+                     G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// Tensor of count ciphertext pairs: d0 = a0 b0, d1 = a0 b1 + a1 b0 into
+// d01 [count][2][lvl][n]; d2 = a1 b1 into d2 [count][lvl][n].
+__global__ void tensor_kernel(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b, unsigned logn,
+                              unsigned lvl, size_t in_stride, size_t in_pstride, size_t d01_stride, size_t d2_stride,
+                              const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned limb = blockIdx.y, c = blockIdx.z;
+  if (i >= n)
+    return;
+  const ModConst m = mc[limb];
+  const size_t off = ((size_t)limb << logn) + i;
+  const uint64_t *pa = a + c * in_stride, *pb = b + c * in_stride;
+  const uint64_t a0 = pa[off], a1 = pa[in_pstride + off], b0 = pb[off], b1 = pb[in_pstride + off];
+  uint64_t *o = d01 + c * d01_stride;
+  o[off] = mul_mod(a0, b0, m);
+  o[((size_t)lvl << logn) + off] = add_mod(mul_mod(a0, b1, m), mul_mod(a1, b0, m), m.q);
+  d2[c * d2_stride + off] = mul_mod(a1, b1, m);
+}
+
+void k_tensor(uint64_t *d01, uint64_t *d2c, const uint64_t *a, const uint64_t *b, unsigned lvl,
+              size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride)
+{
+  hipLaunchKernelGGL(tensor_kernel, dim3((G.n + TPB - 1) / TPB, lvl, count), dim3(TPB), 0, G.stream, d01, d2c, a,
+                     b, G.logn, lvl, in_stride, in_pstride, d_stride, (size_t)lvl << G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void dec_kernel(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned logn,
+                           const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const ModConst m = mc[blockIdx.y];
+  const size_t off = ((size_t)blockIdx.y << logn) + i;
+  pt[off] = add_mod(c0[off], mul_mod(c1[off], s[off], m), m.q);
+}
+
+void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned lvl)
+{
+  hipLaunchKernelGGL(dec_kernel, dim3((G.n + TPB - 1) / TPB, lvl), dim3(TPB), 0, G.stream, pt, c0, c1, s, G.logn,
+                     G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// Small samples (ternary or CBD-21) lifted to every limb of dst.
+__global__ void sample_small_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, int cbd,
+                                    const ModConst *mc)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (1u << logn))
+    return;
+  uint32_t b[16];
+  chacha20_block(b, key, stream, k);
+  int v;
+  if (cbd) {
+    v = __popc(b[0] & 0x1FFFFFu) - __popc(b[1] & 0x1FFFFFu);
+  } else {
+    const uint32_t r = b[0] & 3u;
+    v = r < 2 ? 0 : (r == 2 ? 1 : -1);
+  }
+  for (unsigned l = 0; l < dst.count; l++) {
+    const uint64_t q = mc[dst.mod(l)].q;
+    dst.limb(l, logn)[k] = v >= 0 ? (uint64_t)v : q - (uint64_t)(-v);
+  }
+}
+
+void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd)
+{
+  hipLaunchKernelGGL(sample_small_kernel, grid1(G.n), dim3(TPB), 0, G.stream, dst, G.logn, G.key, stream, cbd,
+                     G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void sample_uniform_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, unsigned nb,
+                                      const ModConst *mc)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (1u << logn))
+    return;
+  const unsigned l = blockIdx.y;
+  const unsigned m = dst.mod(l);
+  const ModConst c = mc[m];
+  uint32_t b[16];
+  chacha20_block(b, key, stream, k * nb + m / 4);
+  const uint32_t *w = b + 4 * (m % 4);
+  const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32), hi = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  // (hi 2^64 + lo) mod q
+  const uint64_t r64 = reduce64(reduce64(~0ull, c) + 1, c);  // 2^64 mod q
+  const uint64_t v = add_mod(mul_mod(reduce64(hi, c), r64, c), reduce64(lo, c), c.q);
+  dst.limb(l, logn)[k] = v;
+}
+
+void k_sample_uniform(const LimbSet &dst, uint64_t stream)
+{
+  const unsigned nb = (G.nmod + 3) / 4;
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3((G.n + TPB - 1) / TPB, dst.count), dim3(TPB), 0, G.stream, dst,
+                     G.logn, G.key, stream, nb, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void lift_i64_kernel(LimbSet dst, const int64_t *coef, unsigned logn, const ModConst *mc)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (1u << logn))
+    return;
+  const unsigned l = blockIdx.y;
+  const ModConst c = mc[dst.mod(l)];
+  const int64_t v = coef[k];
+  uint64_t r;
+  if (v >= 0)
+    r = reduce64((uint64_t)v, c);
+  else
+    r = neg_mod(reduce64((uint64_t)(-(v + 1)), c) + 1 == c.q ? 0 : reduce64((uint64_t)(-(v + 1)), c) + 1, c.q);
+  dst.limb(l, logn)[k] = r;
+}
+
+void k_lift_i64(const LimbSet &dst, const int64_t *coef)
+{
+  hipLaunchKernelGGL(lift_i64_kernel, dim3((G.n + TPB - 1) / TPB, dst.count), dim3(TPB), 0, G.stream, dst, coef,
+                     G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// c0 = v pk0 + e0 + m, c1 = v pk1 + e1 (all NTT domain, lvl limbs).
+__global__ void enc_kernel(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
+                           const uint64_t *pk0, const uint64_t *pk1, const uint64_t *mp, unsigned logn,
+                           const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const ModConst m = mc[blockIdx.y];
+  const size_t o = ((size_t)blockIdx.y << logn) + i;
+  c0[o] = add_mod(add_mod(e0[o], mul_mod(v[o], pk0[o], m), m.q), mp[o], m.q);
+  c1[o] = add_mod(e1[o], mul_mod(v[o], pk1[o], m), m.q);
+}
+
+void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
+                   const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl)
+{
+  hipLaunchKernelGGL(enc_kernel, dim3((G.n + TPB - 1) / TPB, lvl), dim3(TPB), 0, G.stream, c0, c1, v, e0, e1, pk0,
+                     pk1, m, G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// c0 = e - a s + m
+__global__ void enc_sk_kernel(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s,
+                              const uint64_t *mp, unsigned logn, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const ModConst m = mc[blockIdx.y];
+  const size_t o = ((size_t)blockIdx.y << logn) + i;
+  c0[o] = add_mod(sub_mod(e[o], mul_mod(a[o], s[o], m), m.q), mp ? mp[o] : 0, m.q);
+}
+
+void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,
+                      unsigned lvl)
+{
+  hipLaunchKernelGGL(enc_sk_kernel, dim3((G.n + TPB - 1) / TPB, lvl), dim3(TPB), 0, G.stream, c0, a, e, s, m,
+                     G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// evk digit: b = e - a s (+ [P]_q s' on limbs [lo, hi)), all nmod limbs.
+__global__ void evk_kernel(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s,
+                           const uint64_t *sp, unsigned lo, unsigned hi, unsigned logn, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const unsigned l = blockIdx.y;
+  const ModConst m = mc[l];
+  const size_t o = ((size_t)l << logn) + i;
+  uint64_t r = sub_mod(e[o], mul_mod(a[o], s[o], m), m.q);
+  if (l >= lo && l < hi)
+    r = add_mod(r, mul_mod(m.pmod, sp[o], m), m.q);
+  b[o] = r;
+}
+
+void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *sprime,
+                   unsigned lo, unsigned hi)
+{
+  hipLaunchKernelGGL(evk_kernel, dim3((G.n + TPB - 1) / TPB, G.nmod), dim3(TPB), 0, G.stream, b, a, e, s, sprime,
+                     lo, hi, G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__device__ __forceinline__ unsigned auto_index(unsigned k, uint64_t g, unsigned logn)
+{
+  const uint64_t mask = (2ull << logn) - 1;
+  const uint64_t e = ((2ull * brev_dev(k, logn) + 1) * g) & mask;
+  return brev_dev((unsigned)(e >> 1), logn);
+}
+
+__global__ void automorph_kernel(uint64_t *out, const uint64_t *in, unsigned logn, uint64_t g)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const size_t off = (size_t)blockIdx.y << logn;
+  out[off + i] = in[off + auto_index((unsigned)i, g, logn)];
+}
+
+void k_automorph(uint64_t *out, const uint64_t *in, unsigned nlimbs, uint64_t g)
+{
+  hipLaunchKernelGGL(automorph_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs), dim3(TPB), 0, G.stream, out, in,
+                     G.logn, g);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void square_kernel(uint64_t *out, const uint64_t *in, unsigned logn, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const size_t o = ((size_t)blockIdx.y << logn) + i;
+  out[o] = mul_mod(in[o], in[o], mc[blockIdx.y]);
+}
+
+void k_square(uint64_t *out, const uint64_t *in, unsigned nlimbs)
+{
+  hipLaunchKernelGGL(square_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs), dim3(TPB), 0, G.stream, out, in, G.logn,
+                     G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void mul_pt_kernel(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned logn, size_t ps,
+                              const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const ModConst m = mc[blockIdx.y];
+  const size_t o = ((size_t)blockIdx.y << logn) + i;
+  const size_t p = blockIdx.z * ps;
+  out[p + o] = mul_mod(a[p + o], pt[o], m);
+}
+
+void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride)
+{
+  hipLaunchKernelGGL(mul_pt_kernel, dim3((G.n + TPB - 1) / TPB, lvl, 2), dim3(TPB), 0, G.stream, out, a, pt,
+                     G.logn, pstride, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void add_pt_kernel(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned logn, size_t ps,
+                              const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const ModConst m = mc[blockIdx.y];
+  const size_t o = ((size_t)blockIdx.y << logn) + i;
+  out[o] = add_mod(a[o], pt[o], m.q);
+  out[ps + o] = a[ps + o];
+}
+
+void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride)
+{
+  hipLaunchKernelGGL(add_pt_kernel, dim3((G.n + TPB - 1) / TPB, lvl), dim3(TPB), 0, G.stream, out, a, pt, G.logn,
+                     pstride, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// ===========================================================================
+// Basis conversion constants, cached per (kind, level) in device memory.
+// ===========================================================================
+// ModUp table for level lvl, digit j with limbs [lo, hi) (na = hi - lo):
+//   y[i] = [(Qj/q_i)^-1]_{q_i} (+ Shoup)     i in digit
+//   c[i][t] = [Qj/q_i]_{mod_t}               t in basis_qp(lvl)
+struct UpDigit {
+  uint32_t lo, na, pad0, pad1;
+  uint64_t y[8], yp[8];
+};
+
+static unsigned basis_qp(unsigned lvl, unsigned *mods)
+{
+  for (unsigned t = 0; t < lvl; t++)
+    mods[t] = t;
+  for (unsigned k = 0; k < G.K; k++)
+    mods[lvl + k] = G.L + k;
+  return lvl + G.K;
+}
+
+struct UpTable {
+  UpDigit *dig;   // [ndig]
+  uint64_t *c;    // [ndig][8][nm]
+  unsigned ndig, nm;
+};
+
+static std::map<unsigned, UpTable> g_up;
+
+static UpTable &up_table(unsigned lvl)
+{
+  auto it = g_up.find(lvl);
+  if (it != g_up.end())
+    return it->second;
+  if (G.alpha > 8)
+    gpqhe_die("digit size alpha=%u > 8 unsupported", G.alpha);
+  unsigned mods[GPQHE_MAXMOD];
+  const unsigned nm = basis_qp(lvl, mods);
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha;
+  std::vector<UpDigit> dig(ndig);
+  std::vector<uint64_t> c((size_t)ndig * 8 * nm, 0);
+  for (unsigned j = 0; j < ndig; j++) {
+    const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, lvl);
+    dig[j].lo = lo;
+    dig[j].na = hi - lo;
+    for (unsigned i = lo; i < hi; i++) {
+      uint64_t hat = 1;
+      for (unsigned i2 = lo; i2 < hi; i2++)
+        if (i2 != i)
+          hat = hm_mul_mod(hat, G.q[i2] % G.q[i], G.q[i]);
+      dig[j].y[i - lo] = hm_inv_mod(hat, G.q[i]);
+      dig[j].yp[i - lo] = (uint64_t)(((unsigned __int128)dig[j].y[i - lo] << 64) / G.q[i]);
+      for (unsigned t = 0; t < nm; t++) {
+        const uint64_t qt = G.q[mods[t]];
+        uint64_t h = 1;
+        for (unsigned i2 = lo; i2 < hi; i2++)
+          if (i2 != i)
+            h = hm_mul_mod(h, G.q[i2] % qt, qt);
+        c[((size_t)j * 8 + (i - lo)) * nm + t] = h;
+      }
+    }
+  }
+  UpTable tab;
+  tab.ndig = ndig;
+  tab.nm = nm;
+  HIP_CHECK(hipMalloc(&tab.dig, ndig * sizeof(UpDigit)));
+  HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.dig, dig.data(), ndig * sizeof(UpDigit), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.c, c.data(), c.size() * 8, hipMemcpyHostToDevice));
+  return g_up[lvl] = tab;
+}
+
+__device__ __forceinline__ unsigned basis_mod(unsigned t, unsigned lvl, unsigned L)
+{
+  return t < lvl ? t : L + (t - lvl);
+}
+
+// D[p][j][t][k] = FBC(digit j of xc[p]) mod basis_t (coefficient domain);
+// own limbs copy xc (the uniform NTT afterwards reproduces the NTT-domain
+// limb exactly).  grid: (n / TPB, nm, count * ndig).
+__global__ void modup_kernel(uint64_t *D, const uint64_t *xc, unsigned logn, unsigned lvl, unsigned L, unsigned nm,
+                             unsigned ndig, size_t x_stride, size_t d_stride, UpTable tab, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned t = blockIdx.y;
+  const unsigned p = blockIdx.z / ndig, j = blockIdx.z % ndig;
+  // digit constants straight from global memory (wave-uniform -> scalar
+  // loads); a by-value copy indexed by the runtime i would live in scratch
+  const UpDigit *dg = tab.dig + j;
+  const unsigned lo = dg->lo, na = dg->na;
+  const uint64_t *x = xc + p * x_stride;
+  uint64_t *out = D + p * d_stride + (((size_t)j * nm + t) << logn);
+  if (t >= lo && t < lo + na) {
+    out[k] = x[((size_t)t << logn) + k];
+    return;
+  }
+  const ModConst mt = mc[basis_mod(t, lvl, L)];
+  uint64_t acc = 0;
+  for (unsigned i = 0; i < na; i++) {
+    const unsigned li = lo + i;
+    const uint64_t y = mul_shoup(x[((size_t)li << logn) + k], dg->y[i], dg->yp[i], mc[li].q);
+    acc = add_mod(acc, mul_mod(reduce64(y, mt), tab.c[((size_t)j * 8 + i) * nm + t], mt), mt.q);
+  }
+  out[k] = acc;
+}
+
+void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl)
+{
+  UpTable &tab = up_table(lvl);
+  hipLaunchKernelGGL(modup_kernel, dim3((G.n + TPB - 1) / TPB, tab.nm, count * tab.ndig), dim3(TPB), 0, G.stream,
+                     D, xc, G.logn, lvl, G.L, tab.nm, tab.ndig, x_stride, d_stride, tab, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// Key-switch inner product (NTT domain, basis_qp(lvl)):
+//   s0 = sum_j D_j[t][perm k] evk_b[j][t][k] + [P] c0[t][perm k]  (t < lvl)
+//   s1 = sum_j D_j[t][perm k] evk_a[j][t][k] + [P] c1[t][perm k]  (t < lvl)
+// evk == null skips the digit sum; accumulate: acc += pt * s, else acc = s.
+// grid: (n / TPB, nm, count).
+__global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn, unsigned lvl, unsigned L,
+                                unsigned nm, unsigned nmod, unsigned ndig, size_t d_stride, size_t acc_stride,
+                                const uint64_t *evk, uint64_t g, const uint64_t *c0, const uint64_t *c1,
+                                size_t c_stride, size_t c_pstride, const uint64_t *pt, int accumulate,
+                                const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned t = blockIdx.y, p = blockIdx.z;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mm = mc[m];
+  const size_t src = g == 1 ? k : auto_index((unsigned)k, g, logn);
+  uint64_t s0 = 0, s1 = 0;
+  if (evk) {
+    const uint64_t *d = D + p * d_stride + ((size_t)t << logn) + src;
+    for (unsigned j = 0; j < ndig; j++) {
+      const uint64_t dv = d[((size_t)j * nm) << logn];
+      const uint64_t *eb = evk + (((size_t)(2 * j) * nmod + m) << logn);
+      const uint64_t *ea = evk + (((size_t)(2 * j + 1) * nmod + m) << logn);
+      s0 = add_mod(s0, mul_mod(dv, eb[k], mm), mm.q);
+      s1 = add_mod(s1, mul_mod(dv, ea[k], mm), mm.q);
+    }
+  }
+  if (t < lvl) {
+    if (c0)
+      s0 = add_mod(s0, mul_shoup(c0[p * c_stride + ((size_t)t << logn) + src], mm.pmod, mm.pmodp, mm.q), mm.q);
+    if (c1)
+      s1 = add_mod(s1, mul_shoup(c1[p * c_stride + ((size_t)t << logn) + src], mm.pmod, mm.pmodp, mm.q), mm.q);
+  }
+  uint64_t *o0 = acc0 + p * acc_stride + ((size_t)t << logn) + k;
+  uint64_t *o1 = o0 + ((size_t)nm << logn);
+  if (accumulate) {
+    const uint64_t w = pt[((size_t)t << logn) + k];
+    *o0 = add_mod(*o0, mul_mod(w, s0, mm), mm.q);
+    *o1 = add_mod(*o1, mul_mod(w, s1, mm), mm.q);
+  } else {
+    *o0 = s0;
+    *o1 = s1;
+  }
+  (void)c_pstride;
+}
+
+// acc layout per ciphertext p: acc0 at acc + p*acc_stride, acc1 right after
+// it (nm limbs later).
+void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_stride, size_t acc_stride,
+                const uint64_t *evk, unsigned lvl, uint64_t g, const uint64_t *c0, const uint64_t *c1,
+                size_t c_stride, const uint64_t *pt, bool accumulate)
+{
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  hipLaunchKernelGGL(ks_inner_kernel, dim3((G.n + TPB - 1) / TPB, nm, count), dim3(TPB), 0, G.stream, acc, D,
+                     G.logn, lvl, G.L, nm, G.nmod, ndig, d_stride, acc_stride, evk, g, c0, c1, c_stride,
+                     (size_t)0, pt, accumulate ? 1 : 0, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+// ModDown table: divide by the product of the drop moduli (basis positions
+// [keep, nm)), keep basis positions [0, keep).
+struct DownTable {
+  uint64_t *y, *yp;  // [nd]        [(Dprod/d)^-1]_d
+  uint64_t *c;       // [nd][keep]  [Dprod/d]_t
+  uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
+  unsigned keep, nd;
+};
+
+static std::map<std::pair<unsigned, int>, DownTable> g_down;
+
+// mode 0: basis_qp(lvl) / P -> q_0..q_{lvl-1}         (key switching)
+// mode 1: basis_qp(lvl) / (q_{lvl-1} P) -> q_0..q_{lvl-2} (fused rescale)
+// mode 2: q_0..q_{lvl-1} / q_{lvl-1} -> q_0..q_{lvl-2}  (plain rescale)
+static DownTable &down_table(unsigned lvl, int mode)
+{
+  auto key = std::make_pair(lvl, mode);
+  auto it = g_down.find(key);
+  if (it != g_down.end())
+    return it->second;
+  unsigned mods[GPQHE_MAXMOD];
+  const unsigned nm = mode == 2 ? lvl : basis_qp(lvl, mods);
+  if (mode == 2)
+    for (unsigned t = 0; t < lvl; t++)
+      mods[t] = t;
+  const unsigned keep = mode == 0 ? lvl : lvl - 1, nd = nm - keep;
+  std::vector<uint64_t> y(nd), yp(nd), c((size_t)nd * keep), dinv(keep), dinvp(keep);
+  for (unsigned d = 0; d < nd; d++) {
+    const uint64_t qd = G.q[mods[keep + d]];
+    uint64_t hat = 1;
+    for (unsigned d2 = 0; d2 < nd; d2++)
+      if (d2 != d)
+        hat = hm_mul_mod(hat, G.q[mods[keep + d2]] % qd, qd);
+    y[d] = hm_inv_mod(hat, qd);
+    yp[d] = (uint64_t)(((unsigned __int128)y[d] << 64) / qd);
+    for (unsigned t = 0; t < keep; t++) {
+      const uint64_t qt = G.q[mods[t]];
+      uint64_t h = 1;
+      for (unsigned d2 = 0; d2 < nd; d2++)
+        if (d2 != d)
+          h = hm_mul_mod(h, G.q[mods[keep + d2]] % qt, qt);
+      c[(size_t)d * keep + t] = h;
+    }
+  }
+  for (unsigned t = 0; t < keep; t++) {
+    const uint64_t qt = G.q[mods[t]];
+    uint64_t dp = 1;
+    for (unsigned d = 0; d < nd; d++)
+      dp = hm_mul_mod(dp, G.q[mods[keep + d]] % qt, qt);
+    dinv[t] = hm_inv_mod(dp, qt);
+    dinvp[t] = (uint64_t)(((unsigned __int128)dinv[t] << 64) / qt);
+  }
+  DownTable tab;
+  tab.keep = keep;
+  tab.nd = nd;
+  HIP_CHECK(hipMalloc(&tab.y, nd * 8));
+  HIP_CHECK(hipMalloc(&tab.yp, nd * 8));
+  HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
+  HIP_CHECK(hipMalloc(&tab.dinv, keep * 8));
+  HIP_CHECK(hipMalloc(&tab.dinvp, keep * 8));
+  HIP_CHECK(hipMemcpy(tab.y, y.data(), nd * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.yp, yp.data(), nd * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.c, c.data(), c.size() * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.dinv, dinv.data(), keep * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.dinvp, dinvp.data(), keep * 8, hipMemcpyHostToDevice));
+  return g_down[key] = tab;
+}
+
+// conv[p][t][k] = sum_d y_d(x_d[k]) [Dprod/d]_t  (coefficient domain).
+// grid: (n / TPB, keep, npoly)
+__global__ void down_conv_kernel(uint64_t *conv, const uint64_t *X, unsigned logn, unsigned lvl, unsigned L,
+                                 size_t x_pstride, DownTable tab, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned t = blockIdx.y, p = blockIdx.z;
+  const ModConst mt = mc[basis_mod(t, lvl, L)];
+  const uint64_t *x = X + p * x_pstride;
+  uint64_t acc = 0;
+  for (unsigned d = 0; d < tab.nd; d++) {
+    const unsigned bd = tab.keep + d;
+    const uint64_t qd = mc[basis_mod(bd, lvl, L)].q;
+    const uint64_t y = mul_shoup(x[((size_t)bd << logn) + k], tab.y[d], tab.yp[d], qd);
+    acc = add_mod(acc, mul_mod(reduce64(y, mt), tab.c[(size_t)d * tab.keep + t], mt), mt.q);
+  }
+  conv[(((size_t)p * tab.keep + t) << logn) + k] = acc;
+}
+
+// out[p][t] = (X[p][t] - conv[p][t]) * Dprod^-1
+__global__ void down_combine_kernel(uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
+                                    const uint64_t *conv, unsigned logn, unsigned lvl, unsigned L, DownTable tab,
+                                    const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned t = blockIdx.y, p = blockIdx.z;
+  const uint64_t q = mc[basis_mod(t, lvl, L)].q;
+  const size_t o = ((size_t)t << logn) + k;
+  const uint64_t v = sub_mod(X[p * x_pstride + o], conv[(((size_t)p * tab.keep + t) << logn) + k], q);
+  out[p * out_pstride + o] = mul_shoup(v, tab.dinv[t], tab.dinvp[t], q);
+}
+
+// X: npoly polynomials over basis_qp(lvl) (NTT domain, nm limbs each, stride
+// x_pstride); their drop limbs are overwritten (INTT in place).
+void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
+               int mode)
+{
+  DownTable &tab = down_table(lvl, mode);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  LimbSet ds{};
+  ds.base = X + ((size_t)tab.keep << G.logn);
+  ds.stride = x_pstride;
+  ds.per = tab.nd;
+  ds.count = tab.nd * npoly;
+  for (unsigned d = 0; d < tab.nd; d++)
+    ds.mods[d] = (uint8_t)mods[tab.keep + d];
+  k_ntt(ds, true);
+  uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
+  hipLaunchKernelGGL(down_conv_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream, conv,
+                     X, G.logn, lvl, G.L, x_pstride, tab, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+  LimbSet cs{};
+  cs.base = conv;
+  cs.stride = (size_t)tab.keep * G.n;
+  cs.per = tab.keep;
+  cs.count = tab.keep * npoly;
+  for (unsigned t = 0; t < tab.keep; t++)
+    cs.mods[t] = (uint8_t)mods[t];
+  k_ntt(cs, false);
+  hipLaunchKernelGGL(down_combine_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream,
+                     out, out_pstride, X, x_pstride, conv, G.logn, lvl, G.L, tab, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+  pool_free(conv);
+}
+
+// Benchmark input generator (oracle: poly_fill_uniform).
+__global__ void fill_uniform_kernel(uint64_t *data, unsigned logn, unsigned nlimbs, uint64_t seed,
+                                    const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned m = blockIdx.y;
+  const size_t p = blockIdx.z;
+  const uint64_t base = seed ^ (0x48454354520001ull + m);
+  const uint64_t idx = p * n + k;
+  const uint64_t v = splitmix64_mix(base + (idx + 1) * 0x9E3779B97F4A7C15ull);
+  data[((p * nlimbs + m) << logn) + k] = v % mc[m].q;
+}
+
+void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t seed)
+{
+  for (size_t p0 = 0; p0 < npolys; p0 += 65535) {
+    const size_t cnt = std::min<size_t>(65535, npolys - p0);
+    hipLaunchKernelGGL(fill_uniform_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs, (unsigned)cnt), dim3(TPB), 0,
+                       G.stream, data + p0 * nlimbs * G.n, G.logn, nlimbs, seed, G.dev.mc);
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+// ===========================================================================
+// Tables
+// ===========================================================================
+void tables_upload()
+{
+  const size_t n = G.n, nm = G.nmod;
+  std::vector<uint64_t> tw(nm * n), twp(nm * n), itw(nm * n), itwp(nm * n);
+  for (unsigned m = 0; m < nm; m++) {
+    const uint64_t q = G.q[m], psi = G.psi[m], ipsi = hm_inv_mod(psi, q);
+    // powers in natural order, then permuted by bit reversal
+    std::vector<uint64_t> pw(n), ipw(n);
+    pw[0] = ipw[0] = 1;
+    for (size_t k = 1; k < n; k++) {
+      pw[k] = hm_mul_mod(pw[k - 1], psi, q);
+      ipw[k] = hm_mul_mod(ipw[k - 1], ipsi, q);
+    }
+    for (size_t k = 0; k < n; k++) {
+      const unsigned e = hm_brev((unsigned)k, G.logn);
+      tw[m * n + k] = pw[e];
+      itw[m * n + k] = ipw[e];
+      twp[m * n + k] = (uint64_t)(((unsigned __int128)pw[e] << 64) / q);
+      itwp[m * n + k] = (uint64_t)(((unsigned __int128)ipw[e] << 64) / q);
+    }
+  }
+  HIP_CHECK(hipMalloc(&G.dev.mc, nm * sizeof(ModConst)));
+  HIP_CHECK(hipMalloc(&G.dev.tw, nm * n * 8));
+  HIP_CHECK(hipMalloc(&G.dev.twp, nm * n * 8));
+  HIP_CHECK(hipMalloc(&G.dev.itw, nm * n * 8));
+  HIP_CHECK(hipMalloc(&G.dev.itwp, nm * n * 8));
+  HIP_CHECK(hipMemcpy(G.dev.mc, G.mc, nm * sizeof(ModConst), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(G.dev.tw, tw.data(), nm * n * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(G.dev.twp, twp.data(), nm * n * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(G.dev.itw, itw.data(), nm * n * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(G.dev.itwp, itwp.data(), nm * n * 8, hipMemcpyHostToDevice));
+}
+
+void tables_free()
+{
+  HIP_CHECK(hipFree(G.dev.mc));
+  HIP_CHECK(hipFree(G.dev.tw));
+  HIP_CHECK(hipFree(G.dev.twp));
+  HIP_CHECK(hipFree(G.dev.itw));
+  HIP_CHECK(hipFree(G.dev.itwp));
+  G.dev = DevTables{};
+  for (auto &kv : g_up) {
+    HIP_CHECK(hipFree(kv.second.dig));
+    HIP_CHECK(hipFree(kv.second.c));
+  }
+  g_up.clear();
+  for (auto &kv : g_down) {
+    HIP_CHECK(hipFree(kv.second.y));
+    HIP_CHECK(hipFree(kv.second.yp));
+    HIP_CHECK(hipFree(kv.second.c));
+    HIP_CHECK(hipFree(kv.second.dinv));
+    HIP_CHECK(hipFree(kv.second.dinvp));
+  }
+  g_down.clear();
+}

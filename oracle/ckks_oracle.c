@@ -721,13 +721,19 @@ static void fft_tables(unsigned s, double complex **ksi, unsigned **rot)
   *rot = xmalloc((size_t)s * sizeof(unsigned));
   for (unsigned k = 0; k <= M; k++) {
     double ang = 2.0 * M_PI * (double)k / (double)M;
-    (*ksi)[k] = cos(ang) + sin(ang) * I;
+    (*ksi)[k] = CMPLX(cos(ang), sin(ang));
   }
   unsigned r = 1;
   for (unsigned j = 0; j < s; j++) {
     (*rot)[j] = r;
     r = (unsigned)((5ull * r) % M);
   }
+}
+
+/* explicit (ac - bd, ad + bc): no __muldc3, no contraction -> reproducible */
+static inline double complex cmul(double complex a, double complex b)
+{
+  return CMPLX(creal(a) * creal(b) - cimag(a) * cimag(b), creal(a) * cimag(b) + cimag(a) * creal(b));
 }
 
 static void bitrev_perm(double complex *v, unsigned s)
@@ -755,9 +761,9 @@ static void fft_special_dec(double complex *v, unsigned s)
     for (unsigned i = 0; i < s; i += len)
       for (unsigned j = 0; j < h; j++) {
         unsigned idx = (rot[j] % lq) * (M / lq);
-        double complex a = v[i + j], b = v[i + j + h] * ksi[idx];
-        v[i + j] = a + b;
-        v[i + j + h] = a - b;
+        double complex a = v[i + j], b = cmul(v[i + j + h], ksi[idx]);
+        v[i + j] = CMPLX(creal(a) + creal(b), cimag(a) + cimag(b));
+        v[i + j + h] = CMPLX(creal(a) - creal(b), cimag(a) - cimag(b));
       }
   }
   free(ksi);
@@ -775,15 +781,16 @@ static void fft_special_enc(double complex *v, unsigned s)
     for (unsigned i = 0; i < s; i += len)
       for (unsigned j = 0; j < h; j++) {
         unsigned idx = (lq - rot[j] % lq) * (M / lq);
-        double complex a = v[i + j] + v[i + j + h];
-        double complex b = (v[i + j] - v[i + j + h]) * ksi[idx];
+        double complex x = v[i + j], y = v[i + j + h];
+        double complex a = CMPLX(creal(x) + creal(y), cimag(x) + cimag(y));
+        double complex b = cmul(CMPLX(creal(x) - creal(y), cimag(x) - cimag(y)), ksi[idx]);
         v[i + j] = a;
         v[i + j + h] = b;
       }
   }
   bitrev_perm(v, s);
   for (unsigned i = 0; i < s; i++)
-    v[i] /= (double)s;
+    v[i] = CMPLX(creal(v[i]) / (double)s, cimag(v[i]) / (double)s);
   free(ksi);
   free(rot);
 }
@@ -1168,7 +1175,7 @@ void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
     for (unsigned m = 0; m < nl; m++)
       res[m] = c[(size_t)m * n + (size_t)(k + s) * gap];
     double im = crt_center(res, nl);
-    u[k] = re / pt->scale + (im / pt->scale) * I;
+    u[k] = CMPLX(re / pt->scale, im / pt->scale);
   }
   fft_special_dec(u, s);
   memcpy(z, u, (size_t)s * sizeof(double complex));

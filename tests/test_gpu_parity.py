@@ -1,0 +1,167 @@
+"""Product (libgpqhe.so on MI355X) vs oracle (CPU restatement): bit-exact
+parity of every he_* operation on identical seeded inputs.
+
+Parameter sets:
+  ref   : HECTR's own hectx_init(logn=12, q=2^109, slots=16, Delta=2^50)
+          (reference src/ctr.c:514-518) -> n=4096, L=2, K=1, dnum=2
+  c1    : config 1 sizes, n=2^13, L=4 (dnum=4)
+  hyb   : n=2^13, L=5, K=2, dnum=3 (digits {0,1} {2,3} {4}: exercises the
+          fast basis conversion with alpha > 1, K > 1 and a partial digit;
+          P = 2^118 exceeds every digit modulus, as hybrid switching needs)
+  bench : config 2/3 sizes, n=2^16, L=8, K=1, dnum=8
+Integer results must match exactly; decoded values are compared with the
+closed-loop tolerance of the CSTR test (1e-6 relative, reference achieves
+1e-11).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PARAMS = {
+    "ref": ("init", dict(logn=12, logq=109, slots=16, log_delta=50)),
+    "c1": ("params", dict(logn=13, nlimbs=4, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
+    "hyb": ("params", dict(logn=13, nlimbs=5, nspecial=2, dnum=3, slots=32, q0_bits=58, qi_bits=45,
+                           p_bits=59)),
+    "bench": ("params", dict(logn=16, nlimbs=8, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
+}
+
+
+def init_both(oracle, product, name, seed=1234):
+    kind, kw = PARAMS[name]
+    for e in (oracle, product):
+        if kind == "init":
+            e.init(**kw)
+        else:
+            e.init_params(**kw)
+        e.set_seed(seed)
+    assert oracle.primes == product.primes
+    assert list(oracle.info.psi[:len(oracle.primes)]) == list(product.info.psi[:len(product.primes)])
+
+
+def keys(e, rot=True):
+    pk, sk = e.pk(), e.sk()
+    e.keypair(pk, sk)
+    rk = None
+    if rot:
+        rk = e.evks(e.slots)
+        e.genrk(rk, sk)
+    rlk = e.evk()
+    e.genrlk(rlk, sk)
+    return pk, sk, rk, rlk
+
+
+def same(o, p, a, b):
+    A, B = o.export(a), p.export(b)
+    assert A.shape == B.shape
+    bad = np.argwhere(A != B)
+    assert bad.size == 0, f"{len(bad)} residues differ, first at {bad[0].tolist()}"
+
+
+@pytest.mark.parametrize("name", ["ref", "c1", "hyb", "bench"])
+def test_keys_encrypt_decrypt(oracle, product, name):
+    init_both(oracle, product, name)
+    rot = name != "bench"
+    ko, kp = keys(oracle, rot), keys(product, rot)
+    for a, b in zip(ko, kp):
+        if a is None:
+            continue
+        if hasattr(a, "__len__"):
+            for i in range(1, len(a)):
+                same(oracle, product, a[i], b[i])
+        else:
+            same(oracle, product, a, b)
+    rng = np.random.default_rng(5)
+    z = rng.uniform(-1, 1, oracle.slots) + 1j * rng.uniform(-1, 1, oracle.slots)
+    co, cp = oracle.encrypt(z, ko[0]), product.encrypt(z, kp[0])
+    same(oracle, product, co, cp)
+    zo, zp = oracle.decrypt(co, ko[1]), product.decrypt(cp, kp[1])
+    assert np.array_equal(zo, zp)
+    assert np.abs(zp - z).max() < 1e-6
+
+
+@pytest.mark.parametrize("name", ["ref", "c1", "hyb"])
+def test_evaluation_ops(oracle, product, name):
+    init_both(oracle, product, name)
+    ko, kp = keys(oracle), keys(product)
+    rng = np.random.default_rng(11)
+    s = oracle.slots
+    z1 = rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s)
+    z2 = rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s)
+    M = rng.uniform(-4, 4, (s, s))
+    M[np.abs(M) < 1.0] = 0.0  # some zero entries; keep some diagonals
+    M[:, :] *= (np.add.outer(np.arange(s), -np.arange(s)) % 3 != 1)  # zero whole diagonals
+    res = {}
+    for e, k in ((oracle, ko), (product, kp)):
+        pk, sk, rk, rlk = k
+        a, b = e.encrypt(z1, pk), e.encrypt(z2, pk)
+        out = {}
+        for op in ("add", "sub"):
+            c = e.ct()
+            getattr(e, op)(c, a, b)
+            out[op] = c
+        c = e.ct(); e.copy_ct(c, a); e.neg(c); out["neg"] = c
+        c = e.ct(); e.copy_ct(c, a); e.moddown(c); out["moddown"] = c
+        c = e.ct(); e.rot(c, a, 3, rk); out["rot3"] = c
+        c = e.ct(); e.gemv(c, M.ravel(), a, rk); out["gemv"] = c
+        c = e.ct(); e.mul(c, a, b, rlk); out["mul"] = c
+        c = e.ct(); e.mul_rescale(c, a, b, rlk); out["mul_rescale"] = c
+        c = e.ct(); e.mul(c, a, b, rlk); e.rescale(c); out["mul_then_rescale"] = c
+        res[e.name] = (out, sk)
+    for op in res["oracle"][0]:
+        same(oracle, product, res["oracle"][0][op], res["product"][0][op])
+    # decoded sanity on the product side
+    out, sk = res["product"]
+    expect = {"add": z1 + z2, "sub": z1 - z2, "neg": -z1, "moddown": z1, "rot3": np.roll(z1, -3),
+              "gemv": M @ z1, "mul": z1 * z2, "mul_rescale": z1 * z2, "mul_then_rescale": z1 * z2}
+    for op, want in expect.items():
+        got = product.decrypt(out[op], sk)
+        assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
+
+
+def test_ntt_batch_bitexact(oracle, product):
+    """Config 2 layout at n=2^16, L=8 on a 4-polynomial sample."""
+    import torch
+    init_both(oracle, product, "bench")
+    n, L, npolys = product.n, product.L, 4
+    host = np.zeros(npolys * L * n, dtype=np.uint64)
+    oracle.lib.poly_fill_uniform(host.ctypes.data, npolys, L, 99)
+    dev = torch.empty(npolys * L * n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.poly_fill_uniform(dev.data_ptr(), npolys, L, 99)
+    product.sync()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    oracle.lib.poly_ntt_batch(host.ctypes.data, npolys, L)
+    product.lib.poly_ntt_batch(dev.data_ptr(), npolys, L)
+    product.sync()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    oracle.lib.poly_intt_batch(host.ctypes.data, npolys, L)
+    product.lib.poly_intt_batch(dev.data_ptr(), npolys, L)
+    product.sync()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+
+
+def test_mul_rescale_batch_bitexact(oracle, product):
+    """Config 3 op at n=2^16, L=8 on 3 random-residue ciphertext pairs."""
+    import torch
+    init_both(oracle, product, "bench")
+    n, L, cnt = product.n, product.L, 3
+    for e in (oracle, product):
+        e.set_seed(77)
+    _, _, _, rlk_o = keys(oracle, rot=False)
+    _, _, _, rlk_p = keys(product, rot=False)
+    same(oracle, product, rlk_o, rlk_p)
+    words = cnt * 2 * L * n
+    a = np.zeros(words, dtype=np.uint64); b = np.zeros(words, dtype=np.uint64)
+    oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 1)
+    oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 2)
+    out_o = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
+    import ctypes
+    oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk_o))
+    da = torch.from_numpy(a.view(np.int64)).cuda(); db = torch.from_numpy(b.view(np.int64)).cuda()
+    dout = torch.zeros(out_o.size, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, L, ctypes.byref(rlk_p))
+    product.sync()
+    got = dout.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, out_o), f"{np.count_nonzero(got != out_o)} residues differ"
