@@ -41,9 +41,13 @@ def parse():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--logn", type=int, default=16)
     ap.add_argument("--nlimbs", type=int, default=8)
-    ap.add_argument("--dnum", type=int, default=0)
+    ap.add_argument("--dnum", type=int, default=2,
+                    help="key-switch digits (2: fastest measured at L=8, see DESIGN.md; L: one limb per digit)")
+    ap.add_argument("--nspecial", type=int, default=0, help="special primes K (default: enough for P > digit)")
+    ap.add_argument("--no-cstr", action="store_true", help="skip the encrypted CSTR loop (config 4)")
+    ap.add_argument("--cstr-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-ops", type=int, default=0, help="CPU sample size (default: 4 per thread)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration")
     return ap.parse_args()
 
 
@@ -69,15 +73,15 @@ def main():
     L, logn, B = args.nlimbs, args.logn, args.batch
     n = 1 << logn
     dnum = args.dnum or L
+    K = args.nspecial or special_primes(L, dnum)
     eng = Engine.product()
-    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=60, qi_bits=50, p_bits=60,
+    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=60, qi_bits=50, p_bits=60,
                     seed=1000 + rank)
     stream = torch.cuda.Stream()
     eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
     pk, sk, rlk = eng.pk(), eng.sk(), eng.evk()
     eng.keypair(pk, sk)
     eng.genrlk(rlk, sk)
-    K = eng.K
     in_words, out_words = 2 * L * n, 2 * (L - 1) * n
     a = torch.empty(B * in_words, dtype=torch.int64, device="cuda")
     b = torch.empty_like(a)
@@ -120,10 +124,28 @@ def main():
     evk_bytes = 2 * eng.info.dnum * (L + K) * n * 8
     alg_bytes = (2 * in_words + out_words) * 8 + evk_bytes / B
 
+    # instrumented pass (same steps): per-kernel device time from HIP events on
+    # the engine stream, algorithmic bytes per launch from the library
+    eng.prof_enable(True)
+    ti0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    ti1 = time.perf_counter()
+    stats = eng.prof_collect()
+    eng.prof_enable(False)
+
     result = None
     if rank == 0:
-        from hectr_amd import kprof
-        dom = kprof.dominant_kernel(eng, B=min(B, 64), L=L, logn=logn)
+        dom_name = max(stats, key=lambda k: stats[k][1])
+        launches, tot_us, nbytes = stats[dom_name]
+        achieved = nbytes / tot_us / 1e3  # GB/s
+        dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_us": tot_us / launches,
+               "alg_bytes_per_launch": nbytes / launches,
+               "share_of_step": tot_us / (1e6 * (ti1 - ti0))}
+        kernels = {k: {"launches": v[0], "avg_us": v[1] / v[0], "share": v[1] / (1e6 * (ti1 - ti0)),
+                       "GBs": v[2] / v[1] / 1e3} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
         result = {
             "metric": "ct×ct+relin/sec at N=2^16, L=8 RNS primes; encrypted CSTR-MPC steps/sec",
             "value": value,
@@ -146,14 +168,51 @@ def main():
                             "achieved_GBs": alg_bytes * value / world / 1e9,
                             "frac": alg_bytes * value / world / 1e9 / HBM_PEAK_GBS},
             "roofline": dom,
+            "kernels": kernels,
+            "instrumented_ms_per_step": 1e3 * (ti1 - ti0) / args.steps,
         }
     barrier()
+    if rank == 0 and not args.no_cstr:
+        eng.exit()
+        result["cstr"] = cstr_loop(args.cstr_steps)
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, logn, L, dnum)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
+
+
+def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):
+    """Smallest K with P = prod(p_i) above the largest digit modulus (hybrid
+    key switching needs P > Q_j for its noise bound)."""
+    alpha = -(-L // dnum)
+    digit_bits = q0_bits + (alpha - 1) * qi_bits
+    return max(1, -(-digit_bits // p_bits))
+
+
+def cstr_loop(steps):
+    """Config 4: the encrypted CSTR-MPC closed loop on cuda:0 (HECTR's
+    hectx_init(12, 2^109, slots, 2^50); horizon = steps/10, slots from
+    src/ctr.c:510-511), steps/s end to end (plaintext plant + encrypted
+    regulator, keygen excluded) and its deviation from the plaintext loop."""
+    import numpy as np
+
+    from hectr_amd.cstr import CstrProblem, EncryptedRegulator
+    from hectr_amd.gpqhe import Engine
+    pb = CstrProblem(steps)
+    xp, up = pb.simulate(pb.regulator_plain)
+    eng = Engine.product()
+    reg = EncryptedRegulator(eng, pb, seed=5)
+    t0 = time.perf_counter()
+    x, u = pb.simulate(reg)
+    dt = time.perf_counter() - t0
+    reg.close()
+    eng.exit()
+    rel = float(max(np.max(np.abs(x - xp) / np.abs(xp)), np.max(np.abs(u - up) / np.abs(up))))
+    return {"steps": steps, "horizon": pb.horizon, "slots": pb.slots, "steps_per_s": steps / dt,
+            "regulator_ms_median": 1e3 * float(np.median(reg.timings)), "keygen_s": reg.keygen_s,
+            "max_rel_dev_vs_plaintext": rel}
 
 
 def cpu_baseline(args, logn, L, dnum):
@@ -164,23 +223,30 @@ def cpu_baseline(args, logn, L, dnum):
     from hectr_amd.gpqhe import Engine
     threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
     ora = Engine.oracle()
-    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=60, qi_bits=50, p_bits=60, seed=7)
+    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=args.nspecial or special_primes(L, dnum), slots=64,
+                    q0_bits=60, qi_bits=50, p_bits=60, seed=7)
     pk, sk, rlk = ora.pk(), ora.sk(), ora.evk()
     ora.keypair(pk, sk)
     ora.genrlk(rlk, sk)
     n = 1 << logn
-    cnt = args.cpu_ops or max(8, 4 * threads)
+    cnt = 4 * threads  # a fixed set of pairs, multiplied repeatedly for ~cpu_seconds
     a = np.zeros(cnt * 2 * L * n, dtype=np.uint64)
     b = np.zeros_like(a)
     out = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
     ora.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 11)
     ora.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 12)
-    t0 = time.perf_counter()
-    ora.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk))
-    dt = time.perf_counter() - t0
+    done, t0 = 0, time.perf_counter()
+    while True:
+        ora.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk))
+        done += cnt
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
     ora.exit()
+    cnt = done
     return {"value": cnt / dt, "unit": "ct-mult/s", "cores": threads, "kind": "port",
-            "sample": f"{cnt} ct x ct+relin+rescale ops at N=2^{logn}, L={L} ({dt:.1f} s)"}
+            "sample": f"{cnt} ct x ct+relin+rescale ops at N=2^{logn}, L={L}, dnum={dnum} "
+                      f"({4 * threads} distinct pairs, OpenMP over the batch, {dt:.1f} s)"}
 
 
 if __name__ == "__main__":

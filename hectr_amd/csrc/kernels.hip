@@ -16,6 +16,7 @@
 #include "gpqhe_internal.h"
 
 #include <map>
+#include <string.h>
 #include <tuple>
 
 #define TPB 256
@@ -28,6 +29,97 @@ static inline dim3 grid1(size_t n, unsigned tpb = TPB)
 __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 {
   return __brev(x) >> (32 - bits);
+}
+
+
+// ===========================================================================
+// Live kernel statistics (gpqhe_prof_enable / gpqhe_prof_collect): HIP events
+// around each launch on the engine stream.
+// ===========================================================================
+enum KClass {
+  KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
+  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_COUNT
+};
+static const char *kc_names[KC_COUNT] = {
+  "ntt_whole_kernel<false>", "ntt_whole_kernel<true>", "ntt_cols_kernel<false>", "ntt_rows_kernel<false>",
+  "ntt_rows_kernel<true>", "ntt_cols_kernel<true>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
+  "down_conv_kernel", "down_combine_kernel"};
+
+struct ProfEntry {
+  int cls;
+  hipEvent_t a, b;
+  double bytes;
+};
+static bool g_prof = false;
+static std::vector<ProfEntry> g_prof_entries;
+static std::vector<hipEvent_t> g_ev_pool;
+
+static hipEvent_t prof_event()
+{
+  if (!g_ev_pool.empty()) {
+    hipEvent_t e = g_ev_pool.back();
+    g_ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  HIP_CHECK(hipEventCreate(&e));
+  return e;
+}
+
+struct ProfScope {
+  int cls;
+  double bytes;
+  hipEvent_t a = nullptr;
+  ProfScope(int c, double b) : cls(c), bytes(b)
+  {
+    if (!g_prof)
+      return;
+    a = prof_event();
+    HIP_CHECK(hipEventRecord(a, G.stream));
+  }
+  ~ProfScope()
+  {
+    if (!a)
+      return;
+    hipEvent_t b = prof_event();
+    HIP_CHECK(hipEventRecord(b, G.stream));
+    g_prof_entries.push_back({cls, a, b, bytes});
+  }
+};
+
+extern "C" void gpqhe_prof_enable(int on)
+{
+  g_prof = on != 0;
+}
+
+extern "C" unsigned gpqhe_prof_collect(gpqhe_kstat_t *out, unsigned max)
+{
+  if (G.stream)
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+  double us[KC_COUNT] = {0}, bytes[KC_COUNT] = {0};
+  unsigned cnt[KC_COUNT] = {0};
+  for (const ProfEntry &e : g_prof_entries) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));
+    us[e.cls] += 1e3 * ms;
+    bytes[e.cls] += e.bytes;
+    cnt[e.cls]++;
+    g_ev_pool.push_back(e.a);
+    g_ev_pool.push_back(e.b);
+  }
+  g_prof_entries.clear();
+  unsigned k = 0;
+  for (int c = 0; c < KC_COUNT && k < max; c++) {
+    if (!cnt[c])
+      continue;
+    memset(&out[k], 0, sizeof(out[k]));
+    strncpy(out[k].name, kc_names[c], sizeof(out[k].name) - 1);
+    out[k].launches = cnt[c];
+    out[k].total_us = us[c];
+    out[k].bytes = bytes[c];
+    k++;
+  }
+  return k;
 }
 
 // ===========================================================================
@@ -297,6 +389,7 @@ void k_ntt(const LimbSet &s, bool inverse)
   if (s.count > 65535)
     gpqhe_die("k_ntt: %u limbs in one launch", s.count);
   if (logn <= 12) {
+    ProfScope ps(inverse ? KC_NTT_WHOLE_INV : KC_NTT_WHOLE_FWD, 16.0 * n * s.count);
     if (inverse)
       hipLaunchKernelGGL(ntt_whole_kernel<true>, dim3(1, s.count), dim3(TPB), n * 8, G.stream, s, logn, G.dev);
     else
@@ -309,14 +402,23 @@ void k_ntt(const LimbSet &s, bool inverse)
   const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
   const unsigned rows = n2 >= 512 ? 8 : 16;
   const size_t lds_cols = (size_t)n1 * (COLS + 1) * 8, lds_rows = (size_t)rows * (n2 + 1) * 8;
+  const double pass_bytes = 16.0 * n * s.count;  // each pass reads + writes every limb once
   if (!inverse) {
-    hipLaunchKernelGGL(ntt_cols_kernel<false>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s, logn,
-                       logn1, G.dev);
+    {
+      ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
+      hipLaunchKernelGGL(ntt_cols_kernel<false>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s,
+                         logn, logn1, G.dev);
+    }
+    ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
     hipLaunchKernelGGL(ntt_rows_kernel<false>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
                        logn1, rows, G.dev);
   } else {
-    hipLaunchKernelGGL(ntt_rows_kernel<true>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
-                       logn1, rows, G.dev);
+    {
+      ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
+      hipLaunchKernelGGL(ntt_rows_kernel<true>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
+                         logn1, rows, G.dev);
+    }
+    ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
     hipLaunchKernelGGL(ntt_cols_kernel<true>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s, logn,
                        logn1, G.dev);
   }
@@ -389,6 +491,7 @@ __global__ void tensor_kernel(uint64_t *d01, uint64_t *d2, const uint64_t *a, co
 void k_tensor(uint64_t *d01, uint64_t *d2c, const uint64_t *a, const uint64_t *b, unsigned lvl,
               size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride)
 {
+  ProfScope ps(KC_TENSOR, 8.0 * G.n * lvl * count * 7);  // read 4 limbs, write 3 limbs
   hipLaunchKernelGGL(tensor_kernel, dim3((G.n + TPB - 1) / TPB, lvl, count), dim3(TPB), 0, G.stream, d01, d2c, a,
                      b, G.logn, lvl, in_stride, in_pstride, d_stride, (size_t)lvl << G.logn, G.dev.mc);
   HIP_CHECK(hipGetLastError());
@@ -753,6 +856,7 @@ __global__ void modup_kernel(uint64_t *D, const uint64_t *xc, unsigned logn, uns
 void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl)
 {
   UpTable &tab = up_table(lvl);
+  ProfScope ps(KC_MODUP, 8.0 * G.n * count * (lvl + tab.ndig * tab.nm));
   hipLaunchKernelGGL(modup_kernel, dim3((G.n + TPB - 1) / TPB, tab.nm, count * tab.ndig), dim3(TPB), 0, G.stream,
                      D, xc, G.logn, lvl, G.L, tab.nm, tab.ndig, x_stride, d_stride, tab, G.dev.mc);
   HIP_CHECK(hipGetLastError());
@@ -814,6 +918,11 @@ void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_strid
                 size_t c_stride, const uint64_t *pt, bool accumulate)
 {
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  // reads D and c0/c1 per ciphertext + the evk once, writes 2 nm limbs per ciphertext
+  const double kb = 8.0 * G.n *
+                    ((double)count * (ndig * nm * (evk ? 1 : 0) + (c0 ? lvl : 0) + (c1 ? lvl : 0) +
+                                      (accumulate ? 5 : 2) * nm) + (evk ? 2.0 * ndig * nm : 0));
+  ProfScope ps(KC_KS_INNER, kb);
   hipLaunchKernelGGL(ks_inner_kernel, dim3((G.n + TPB - 1) / TPB, nm, count), dim3(TPB), 0, G.stream, acc, D,
                      G.logn, lvl, G.L, nm, G.nmod, ndig, d_stride, acc_stride, evk, g, c0, c1, c_stride,
                      (size_t)0, pt, accumulate ? 1 : 0, G.dev.mc);
@@ -943,9 +1052,12 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
     ds.mods[d] = (uint8_t)mods[tab.keep + d];
   k_ntt(ds, true);
   uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
+  {
+  ProfScope ps(KC_DOWN_CONV, 8.0 * G.n * npoly * (tab.nd + tab.keep));
   hipLaunchKernelGGL(down_conv_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream, conv,
                      X, G.logn, lvl, G.L, x_pstride, tab, G.dev.mc);
   HIP_CHECK(hipGetLastError());
+  }
   LimbSet cs{};
   cs.base = conv;
   cs.stride = (size_t)tab.keep * G.n;
@@ -954,6 +1066,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
   for (unsigned t = 0; t < tab.keep; t++)
     cs.mods[t] = (uint8_t)mods[t];
   k_ntt(cs, false);
+  ProfScope ps(KC_DOWN_COMBINE, 8.0 * G.n * npoly * tab.keep * 3);
   hipLaunchKernelGGL(down_combine_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream,
                      out, out_pstride, X, x_pstride, conv, G.logn, lvl, G.L, tab, G.dev.mc);
   HIP_CHECK(hipGetLastError());

@@ -329,6 +329,7 @@ class EncryptedRegulator:
         t0 = time.perf_counter()
         engine.keypair(self.pk, self.sk)
         engine.genrk(self.rk, self.sk)
+        engine.sync()
         self.keygen_s = time.perf_counter() - t0
         self.ct = {k: engine.ct() for k in ("xhat", "uhat", "xr", "ur", "up")}
         self.MAz = d2z_matrix(problem.MA, s).ravel()

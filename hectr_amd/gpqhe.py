@@ -75,6 +75,11 @@ class Info(C.Structure):
     ]
 
 
+class KStat(C.Structure):
+    _fields_ = [("name", C.c_char * 40), ("launches", C.c_uint32), ("reserved", C.c_uint32),
+                ("total_us", C.c_double), ("bytes", C.c_double)]
+
+
 P = C.POINTER
 OBJ = P(HeObject)
 VP = C.c_void_p
@@ -128,6 +133,8 @@ SIGNATURES = {
     "he_export": (C.c_size_t, [VP, U64P]),
     "he_import": (None, [VP, U64P, C.c_uint, C.c_double, C.c_uint32]),
     "he_evk_meta": (None, [OBJ, P(C.c_uint32), P(C.c_uint32)]),
+    "gpqhe_prof_enable": (None, [C.c_int]),
+    "gpqhe_prof_collect": (C.c_uint, [P(KStat), C.c_uint]),
 }
 
 #: symbols declared in include/gpqhe.h (checked by tests/test_abi.py)
@@ -198,6 +205,15 @@ class Engine:
 
     def sync(self):
         self.lib.gpqhe_sync()
+
+    def prof_enable(self, on=True):
+        self.lib.gpqhe_prof_enable(1 if on else 0)
+
+    def prof_collect(self):
+        """{kernel: (launches, total_us, algorithmic bytes)}; resets the counters."""
+        buf = (KStat * 64)()
+        k = self.lib.gpqhe_prof_collect(buf, 64)
+        return {buf[i].name.decode(): (buf[i].launches, buf[i].total_us, buf[i].bytes) for i in range(k)}
 
     # ------------------------------------------------------------ objects
     def _new(self, kind: str) -> HeObject:

@@ -202,6 +202,23 @@ void poly_intt_batch(uint64_t *data, size_t npolys, unsigned int nlimbs);
 void poly_fill_uniform(uint64_t *data, size_t npolys, unsigned int nlimbs, uint64_t seed);
 
 /* ------------------------------------------------------------------------ */
+/* [ext] Live kernel statistics: when enabled, every kernel launch is        */
+/* bracketed by HIP events on the engine stream; collect returns, per kernel */
+/* class (one kernel symbol each), launches, device time and algorithmic     */
+/* bytes (bytes the launch must read + write at minimum), then resets.       */
+/* The oracle returns 0 classes.                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct gpqhe_kstat {
+  char     name[40];
+  uint32_t launches;
+  uint32_t reserved;
+  double   total_us;
+  double   bytes;
+} gpqhe_kstat_t;
+void     gpqhe_prof_enable(int on);
+unsigned gpqhe_prof_collect(gpqhe_kstat_t *out, unsigned max);
+
+/* ------------------------------------------------------------------------ */
 /* [ext] Serialization (host buffers): residues in the payload layout above, */
 /* npoly x nlimbs x n words.  Used for fixtures and cross-engine parity.     */
 /* ------------------------------------------------------------------------ */

@@ -455,6 +455,18 @@ void gpqhe_sync(void)
 {
 }
 
+void gpqhe_prof_enable(int on)
+{
+  (void)on;
+}
+
+unsigned gpqhe_prof_collect(gpqhe_kstat_t *out, unsigned max)
+{
+  (void)out;
+  (void)max;
+  return 0;
+}
+
 /* ======================================================================== */
 /* NTT (negacyclic, merged psi; CT forward natural->bit-reversed, GS inverse */
 /* bit-reversed->natural).  Output index k holds a(psi^(2 brev(k) + 1)).     */
