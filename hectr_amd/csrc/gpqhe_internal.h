@@ -37,7 +37,10 @@ struct ModConst {
   uint32_t pad;
   uint64_t ninv, ninvp;  // n^-1 and Shoup companion
   uint64_t pmod, pmodp;  // [P]_q (product of the special primes) + Shoup
+  uint64_t qneg_inv;     // -q^-1 mod 2^64 (Montgomery REDC)
+  uint64_t r64;          // 2^64 mod q
 };
+
 
 // ---------------------------------------------------------------------------
 // Modular arithmetic (host + device).
@@ -91,6 +94,16 @@ __host__ __device__ __forceinline__ uint64_t mul_shoup(uint64_t a, uint64_t w, u
 __host__ __device__ __forceinline__ uint64_t mul_shoup_lazy(uint64_t a, uint64_t w, uint64_t wp, uint64_t q)
 {
   return a * w - mulhi64(a, wp) * q;
+}
+
+// Montgomery REDC of a 128-bit (hi:lo) sum v < 8 q 2^61: returns v 2^-64 mod q
+// (canonical).  Used with constants pre-multiplied by 2^64 so the result is
+// the plain residue.
+__host__ __device__ __forceinline__ uint64_t redc128(uint64_t hi, uint64_t lo, const ModConst &m)
+{
+  const uint64_t mq = lo * m.qneg_inv;
+  uint64_t t = hi + mulhi64(mq, m.q) + (lo != 0);
+  return t >= m.q ? t - m.q : t;
 }
 
 // x mod q for arbitrary 64-bit x (q < 2^61): reduce via Barrett on (0:x).
@@ -188,6 +201,7 @@ struct Context {
   ChachaKey key;
   uint64_t counter = 0;
   DevTables dev{};
+  const uint64_t *tw2 = nullptr, *itw2 = nullptr;  // interleaved (w, w') pairs [nmod][n][2]
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;
   int device = 0;

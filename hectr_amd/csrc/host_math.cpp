@@ -60,6 +60,11 @@ void hm_modconst(ModConst &m, uint64_t q)
   m.q = q;
   m.k = 64 - (unsigned)__builtin_clzll(q);
   m.mu = (uint64_t)(((u128)1 << (2 * m.k)) / q);
+  uint64_t inv = 1;  // q^-1 mod 2^64 by Newton iteration (q odd)
+  for (int i = 0; i < 6; i++)
+    inv *= 2 - q * inv;
+  m.qneg_inv = (uint64_t)0 - inv;
+  m.r64 = (uint64_t)(((u128)1 << 64) % q);
 }
 
 static bool is_prime64(uint64_t n)

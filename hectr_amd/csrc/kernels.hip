@@ -381,6 +381,275 @@ __global__ void __launch_bounds__(TPB) ntt_rows_kernel(LimbSet s, unsigned logn,
   }
 }
 
+
+// ===========================================================================
+// NTT v2 (two-pass, n = 2^13 .. 2^16): 4096-element tiles, 256 threads,
+// Harvey lazy butterflies (values in [0, 4q) inside a pass, canonical at every
+// pass boundary), interleaved (w, w') twiddle pairs (one 16-byte load), round
+// A loaded straight from HBM into registers, prime-major workgroup order so
+// the workgroups resident at one time share one prime's twiddle table.
+// ===========================================================================
+struct Tw2 {
+  const uint64_t *fwd;  // [nmod][n][2]
+  const uint64_t *inv;
+};
+
+__device__ __forceinline__ uint64_t lazy_lt2q(uint64_t x, uint64_t q2)
+{
+  return x >= q2 ? x - q2 : x;
+}
+
+__device__ __forceinline__ uint64_t canon4(uint64_t x, uint64_t q, uint64_t q2)
+{
+  x = x >= q2 ? x - q2 : x;
+  return x >= q ? x - q : x;
+}
+
+// forward CT stages on E = 2^LE registers; twiddle run of stage s starts at
+// bb >> (log_thi - s + 1); inputs < 4q, outputs < 4q
+template <int LE>
+__device__ __forceinline__ void fwd_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
+                                           int log_thi, uint64_t q)
+{
+  constexpr int E = 1 << LE;
+  const uint64_t q2 = 2 * q;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_thi - s + 1);
+    const int half = E >> (s + 1);
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
+      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
+      const uint64_t U = lazy_lt2q(x[k], q2);
+      const uint64_t V = mul_shoup_lazy(x[k + half], w, wp, q);
+      x[k] = U + V;
+      x[k + half] = U - V + q2;
+    }
+  }
+}
+
+// inverse GS stages; inputs < 2q, outputs < 2q
+template <int LE>
+__device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
+                                           int log_tlo, uint64_t q)
+{
+  constexpr int E = 1 << LE;
+  const uint64_t q2 = 2 * q;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_tlo + s + 1);
+    const int half = 1 << s;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
+      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
+      const uint64_t U = x[k], V = x[k + half];
+      x[k] = lazy_lt2q(U + V, q2);
+      x[k + half] = mul_shoup_lazy(U - V + q2, w, wp, q);
+    }
+  }
+}
+
+// block -> (limb, tile) in prime-major order: all tiles of all limbs that use
+// basis slot t run before slot t + 1.
+__device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsigned &v, unsigned &tile)
+{
+  const unsigned groups = s.count / s.per;
+  const unsigned b = blockIdx.x;
+  const unsigned t = b / (groups * tiles);
+  const unsigned rem = b - t * groups * tiles;
+  const unsigned grp = rem / tiles;
+  tile = rem - grp * tiles;
+  v = grp * s.per + t;
+}
+
+// Column pass: tile = T rows x C columns (T C = 4096).
+template <int LOGT, bool INV>
+__global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, unsigned logn, Tw2 tw, const ModConst *mcs)
+{
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
+  const unsigned n2 = 1u << (logn - LOGT);
+  unsigned v, tile;
+  pm_decode(s, n2 / C, v, tile);
+  const unsigned m = s.mod(v);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  uint64_t *x = s.limb(v, logn) + (size_t)tile * C;
+  const int t = threadIdx.x;
+  if constexpr (!INV) {
+    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+    // round A: rows l + 16 k (distances T/2 .. 16)
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = x[(size_t)(l + 16 * k) * n2 + c];
+      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        lds[(l + 16 * k) * CP + c] = r[k];
+    }
+    __syncthreads();
+    // round B: rows 16 g + k (distances 8 .. 1)
+    {
+      const int c = t % C, g = t / C;
+      uint64_t r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = lds[(16 * g + k) * CP + c];
+      fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        x[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+    }
+  } else {
+    const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
+    {
+      const int c = t % C, g = t / C;
+      uint64_t r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = x[(size_t)(16 * g + k) * n2 + c];
+      inv_stages<4>(r, tw2, T + 16 * g, 0, q);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[(16 * g + k) * CP + c] = r[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = lds[(l + 16 * k) * CP + c];
+      inv_stages<LEA>(r, tw2, T, 4, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        x[(size_t)(l + 16 * k) * n2 + c] = mul_shoup(r[k], mc.ninv, mc.ninvp, q);
+    }
+  }
+}
+
+// Row pass: tile = R rows x N2 columns (R N2 = 4096).
+template <int LOGN2, bool INV>
+__global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn, Tw2 tw, const ModConst *mcs)
+{
+  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  unsigned v, tile;
+  pm_decode(s, n1 / R, v, tile);
+  const unsigned m = s.mod(v);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * R;
+  uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
+  const int t = threadIdx.x;
+  if constexpr (!INV) {
+    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+#pragma unroll
+    for (int it = 0; it < R / 16; it++) {
+      const int item = t + 256 * it, l = item % 16, rr = item / 16;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = x[(rr << LOGN2) + l + 16 * k];
+      fwd_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, LOGN2 - 1, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        lds[rr * SP + l + 16 * k] = r[k];
+    }
+    __syncthreads();
+    {
+      const int g = t % (N2 / 16), rr = t / (N2 / 16);
+      uint64_t r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = lds[rr * SP + 16 * g + k];
+      fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[rr * SP + 16 * g + k] = canon4(r[k], q, q2);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int e = t + 256 * i;
+      x[e] = lds[(e >> LOGN2) * SP + (e & (N2 - 1))];
+    }
+  } else {
+    const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int e = t + 256 * i;
+      lds[(e >> LOGN2) * SP + (e & (N2 - 1))] = x[e];
+    }
+    __syncthreads();
+    {
+      const int g = t % (N2 / 16), rr = t / (N2 / 16);
+      uint64_t r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = lds[rr * SP + 16 * g + k];
+      inv_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[rr * SP + 16 * g + k] = r[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < R / 16; it++) {
+      const int item = t + 256 * it, l = item % 16, rr = item / 16;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = lds[rr * SP + l + 16 * k];
+      inv_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, 4, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        x[(rr << LOGN2) + l + 16 * k] = canon4(r[k], q, q2);
+    }
+  }
+}
+
+template <int LOGT1, int LOGN2>
+static void ntt2_launch(const LimbSet &s, bool inverse)
+{
+  const unsigned logn = G.logn, n = G.n;
+  const unsigned blocks = s.count * (n / 4096);
+  const Tw2 tw{G.tw2, G.itw2};
+  const double pass_bytes = 16.0 * n * s.count;
+  if (!inverse) {
+    {
+      ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
+      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+                         G.dev.mc);
+    }
+    ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
+    hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+                       G.dev.mc);
+  } else {
+    {
+      ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
+      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+                         G.dev.mc);
+    }
+    ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
+    hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+                       G.dev.mc);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
 void k_ntt(const LimbSet &s, bool inverse)
 {
   if (!s.count)
@@ -396,6 +665,15 @@ void k_ntt(const LimbSet &s, bool inverse)
       hipLaunchKernelGGL(ntt_whole_kernel<false>, dim3(1, s.count), dim3(TPB), n * 8, G.stream, s, logn, G.dev);
     HIP_CHECK(hipGetLastError());
     return;
+  }
+  if (!getenv("GPQHE_NTT_V1")) {
+    switch (logn) {
+    case 13: ntt2_launch<6, 7>(s, inverse); return;
+    case 14: ntt2_launch<7, 7>(s, inverse); return;
+    case 15: ntt2_launch<7, 8>(s, inverse); return;
+    case 16: ntt2_launch<8, 8>(s, inverse); return;
+    default: break;
+    }
   }
   const unsigned logn1 = logn / 2;  // 13:6x7 14:7x7 15:7x8 16:8x8 17:8x9
   const unsigned logn2 = logn - logn1;
@@ -802,7 +1080,7 @@ static UpTable &up_table(unsigned lvl)
         for (unsigned i2 = lo; i2 < hi; i2++)
           if (i2 != i)
             h = hm_mul_mod(h, G.q[i2] % qt, qt);
-        c[((size_t)j * 8 + (i - lo)) * nm + t] = h;
+        c[((size_t)j * 8 + (i - lo)) * nm + t] = hm_mul_mod(h, G.mc[mods[t]].r64, qt);  // Montgomery form
       }
     }
   }
@@ -823,7 +1101,10 @@ __device__ __forceinline__ unsigned basis_mod(unsigned t, unsigned lvl, unsigned
 
 // D[p][j][t][k] = FBC(digit j of xc[p]) mod basis_t (coefficient domain);
 // own limbs copy xc (the uniform NTT afterwards reproduces the NTT-domain
-// limb exactly).  grid: (n / TPB, nm, count * ndig).
+// limb exactly).  One thread per coefficient walks every target: the digit's
+// y_i = x_i [(Qj/q_i)^-1] are formed once, each target sums y_i [Qj/q_i]_t
+// 2^64 lazily in 128 bits and pays one Montgomery REDC.
+// grid: (n / TPB, ndig, count).
 __global__ void modup_kernel(uint64_t *D, const uint64_t *xc, unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                              unsigned ndig, size_t x_stride, size_t d_stride, UpTable tab, const ModConst *mc)
 {
@@ -831,34 +1112,40 @@ __global__ void modup_kernel(uint64_t *D, const uint64_t *xc, unsigned logn, uns
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n)
     return;
-  const unsigned t = blockIdx.y;
-  const unsigned p = blockIdx.z / ndig, j = blockIdx.z % ndig;
-  // digit constants straight from global memory (wave-uniform -> scalar
-  // loads); a by-value copy indexed by the runtime i would live in scratch
+  const unsigned j = blockIdx.y, p = blockIdx.z;
   const UpDigit *dg = tab.dig + j;
   const unsigned lo = dg->lo, na = dg->na;
   const uint64_t *x = xc + p * x_stride;
-  uint64_t *out = D + p * d_stride + (((size_t)j * nm + t) << logn);
-  if (t >= lo && t < lo + na) {
-    out[k] = x[((size_t)t << logn) + k];
-    return;
+  uint64_t *out = D + p * d_stride + (((size_t)j * nm) << logn) + k;
+  uint64_t y[8];
+#pragma unroll
+  for (unsigned i = 0; i < 8; i++)
+    if (i < na)
+      y[i] = mul_shoup(x[((size_t)(lo + i) << logn) + k], dg->y[i], dg->yp[i], mc[lo + i].q);
+  const uint64_t *cj = tab.c + (size_t)j * 8 * nm;
+  for (unsigned t = 0; t < nm; t++) {
+    uint64_t r;
+    if (t >= lo && t < lo + na) {
+      r = x[((size_t)t << logn) + k];
+    } else {
+      const ModConst mt = mc[basis_mod(t, lvl, L)];
+      unsigned __int128 acc = 0;
+#pragma unroll
+      for (unsigned i = 0; i < 8; i++)
+        if (i < na)
+          acc += (unsigned __int128)y[i] * cj[i * nm + t];
+      r = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mt);
+    }
+    out[(size_t)t << logn] = r;
   }
-  const ModConst mt = mc[basis_mod(t, lvl, L)];
-  uint64_t acc = 0;
-  for (unsigned i = 0; i < na; i++) {
-    const unsigned li = lo + i;
-    const uint64_t y = mul_shoup(x[((size_t)li << logn) + k], dg->y[i], dg->yp[i], mc[li].q);
-    acc = add_mod(acc, mul_mod(reduce64(y, mt), tab.c[((size_t)j * 8 + i) * nm + t], mt), mt.q);
-  }
-  out[k] = acc;
 }
 
 void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl)
 {
   UpTable &tab = up_table(lvl);
   ProfScope ps(KC_MODUP, 8.0 * G.n * count * (lvl + tab.ndig * tab.nm));
-  hipLaunchKernelGGL(modup_kernel, dim3((G.n + TPB - 1) / TPB, tab.nm, count * tab.ndig), dim3(TPB), 0, G.stream,
-                     D, xc, G.logn, lvl, G.L, tab.nm, tab.ndig, x_stride, d_stride, tab, G.dev.mc);
+  hipLaunchKernelGGL(modup_kernel, dim3((G.n + TPB - 1) / TPB, tab.ndig, count), dim3(TPB), 0, G.stream, D, xc,
+                     G.logn, lvl, G.L, tab.nm, tab.ndig, x_stride, d_stride, tab, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -877,7 +1164,9 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n)
     return;
-  const unsigned t = blockIdx.y, p = blockIdx.z;
+  // grid (n/TPB, count, nm): basis slot slowest so one evk limb serves every
+  // ciphertext of the chunk from L2 before the next limb is touched
+  const unsigned p = blockIdx.y, t = blockIdx.z;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mm = mc[m];
   const size_t src = g == 1 ? k : auto_index((unsigned)k, g, logn);
@@ -923,7 +1212,7 @@ void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_strid
                     ((double)count * (ndig * nm * (evk ? 1 : 0) + (c0 ? lvl : 0) + (c1 ? lvl : 0) +
                                       (accumulate ? 5 : 2) * nm) + (evk ? 2.0 * ndig * nm : 0));
   ProfScope ps(KC_KS_INNER, kb);
-  hipLaunchKernelGGL(ks_inner_kernel, dim3((G.n + TPB - 1) / TPB, nm, count), dim3(TPB), 0, G.stream, acc, D,
+  hipLaunchKernelGGL(ks_inner_kernel, dim3((G.n + TPB - 1) / TPB, count, nm), dim3(TPB), 0, G.stream, acc, D,
                      G.logn, lvl, G.L, nm, G.nmod, ndig, d_stride, acc_stride, evk, g, c0, c1, c_stride,
                      (size_t)0, pt, accumulate ? 1 : 0, G.dev.mc);
   HIP_CHECK(hipGetLastError());
@@ -970,7 +1259,7 @@ static DownTable &down_table(unsigned lvl, int mode)
       for (unsigned d2 = 0; d2 < nd; d2++)
         if (d2 != d)
           h = hm_mul_mod(h, G.q[mods[keep + d2]] % qt, qt);
-      c[(size_t)d * keep + t] = h;
+      c[(size_t)d * keep + t] = hm_mul_mod(h, G.mc[mods[t]].r64, qt);  // Montgomery form
     }
   }
   for (unsigned t = 0; t < keep; t++) {
@@ -997,8 +1286,9 @@ static DownTable &down_table(unsigned lvl, int mode)
   return g_down[key] = tab;
 }
 
-// conv[p][t][k] = sum_d y_d(x_d[k]) [Dprod/d]_t  (coefficient domain).
-// grid: (n / TPB, keep, npoly)
+// conv[p][t][k] = sum_d y_d(x_d[k]) [Dprod/d]_t  (coefficient domain); one
+// thread per coefficient walks every keep target (lazy 128-bit sums, REDC).
+// grid: (n / TPB, npoly)
 __global__ void down_conv_kernel(uint64_t *conv, const uint64_t *X, unsigned logn, unsigned lvl, unsigned L,
                                  size_t x_pstride, DownTable tab, const ModConst *mc)
 {
@@ -1006,17 +1296,25 @@ __global__ void down_conv_kernel(uint64_t *conv, const uint64_t *X, unsigned log
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n)
     return;
-  const unsigned t = blockIdx.y, p = blockIdx.z;
-  const ModConst mt = mc[basis_mod(t, lvl, L)];
+  const unsigned p = blockIdx.y;
   const uint64_t *x = X + p * x_pstride;
-  uint64_t acc = 0;
-  for (unsigned d = 0; d < tab.nd; d++) {
-    const unsigned bd = tab.keep + d;
-    const uint64_t qd = mc[basis_mod(bd, lvl, L)].q;
-    const uint64_t y = mul_shoup(x[((size_t)bd << logn) + k], tab.y[d], tab.yp[d], qd);
-    acc = add_mod(acc, mul_mod(reduce64(y, mt), tab.c[(size_t)d * tab.keep + t], mt), mt.q);
+  uint64_t y[8];
+#pragma unroll
+  for (unsigned d = 0; d < 8; d++)
+    if (d < tab.nd) {
+      const unsigned bd = tab.keep + d;
+      y[d] = mul_shoup(x[((size_t)bd << logn) + k], tab.y[d], tab.yp[d], mc[basis_mod(bd, lvl, L)].q);
+    }
+  uint64_t *o = conv + (((size_t)p * tab.keep) << logn) + k;
+  for (unsigned t = 0; t < tab.keep; t++) {
+    const ModConst mt = mc[basis_mod(t, lvl, L)];
+    unsigned __int128 acc = 0;
+#pragma unroll
+    for (unsigned d = 0; d < 8; d++)
+      if (d < tab.nd)
+        acc += (unsigned __int128)y[d] * tab.c[(size_t)d * tab.keep + t];
+    o[(size_t)t << logn] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mt);
   }
-  conv[(((size_t)p * tab.keep + t) << logn) + k] = acc;
 }
 
 // out[p][t] = (X[p][t] - conv[p][t]) * Dprod^-1
@@ -1054,7 +1352,9 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
   uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   {
   ProfScope ps(KC_DOWN_CONV, 8.0 * G.n * npoly * (tab.nd + tab.keep));
-  hipLaunchKernelGGL(down_conv_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream, conv,
+  if (tab.nd > 8)
+    gpqhe_die("ModDown over %u moduli unsupported (max 8)", tab.nd);
+  hipLaunchKernelGGL(down_conv_kernel, dim3((G.n + TPB - 1) / TPB, npoly), dim3(TPB), 0, G.stream, conv,
                      X, G.logn, lvl, G.L, x_pstride, tab, G.dev.mc);
   HIP_CHECK(hipGetLastError());
   }
@@ -1133,6 +1433,17 @@ void tables_upload()
   HIP_CHECK(hipMemcpy(G.dev.twp, twp.data(), nm * n * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(G.dev.itw, itw.data(), nm * n * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(G.dev.itwp, itwp.data(), nm * n * 8, hipMemcpyHostToDevice));
+  std::vector<uint64_t> f2(2 * nm * n), i2(2 * nm * n);
+  for (size_t k = 0; k < nm * n; k++) {
+    f2[2 * k] = tw[k];
+    f2[2 * k + 1] = twp[k];
+    i2[2 * k] = itw[k];
+    i2[2 * k + 1] = itwp[k];
+  }
+  HIP_CHECK(hipMalloc((void **)&G.tw2, 2 * nm * n * 8));
+  HIP_CHECK(hipMalloc((void **)&G.itw2, 2 * nm * n * 8));
+  HIP_CHECK(hipMemcpy((void *)G.tw2, f2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy((void *)G.itw2, i2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
 }
 
 void tables_free()
@@ -1142,6 +1453,9 @@ void tables_free()
   HIP_CHECK(hipFree(G.dev.twp));
   HIP_CHECK(hipFree(G.dev.itw));
   HIP_CHECK(hipFree(G.dev.itwp));
+  HIP_CHECK(hipFree((void *)G.tw2));
+  HIP_CHECK(hipFree((void *)G.itw2));
+  G.tw2 = G.itw2 = nullptr;
   G.dev = DevTables{};
   for (auto &kv : g_up) {
     HIP_CHECK(hipFree(kv.second.dig));
