@@ -57,18 +57,13 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from hectr_amd import dist as hdist
     from hectr_amd.gpqhe import Engine
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = hdist.env()
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
+    hdist.init("nccl")
+    barrier = hdist.barrier
 
     L, logn, B = args.nlimbs, args.logn, args.batch
     n = 1 << logn
@@ -87,8 +82,8 @@ def main():
     b = torch.empty_like(a)
     out = torch.empty(B * out_words, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
-    eng.lib.poly_fill_uniform(a.data_ptr(), 2 * B, L, 11 + 2 * rank)
-    eng.lib.poly_fill_uniform(b.data_ptr(), 2 * B, L, 12 + 2 * rank)
+    # global pairs [rank B, (rank + 1) B): each rank multiplies its own shard
+    hdist.fill_pairs(eng.lib, a.data_ptr(), b.data_ptr(), rank * B, B, L, n)
     eng.sync()
 
     def step():
@@ -112,10 +107,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     ev_s = ev0.elapsed_time(ev1) / 1e3
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = hdist.max_over_ranks(elapsed, device="cuda")
     ops = world * B * args.steps
     value = ops / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
@@ -181,6 +173,7 @@ def main():
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
+    return result
 
 
 def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):

@@ -451,7 +451,24 @@ extern "C" void he_alloc_evk(he_evk_t *evk)
   memset(evk, 0, sizeof(*evk));
 }
 
-extern "C" void he_free_evk(he_evk_t *evk) { obj_free(evk); }
+// Montgomery-form shadow of a key (x 2^64 mod q), kept in `reserved`, used by
+// the fused key-switch inner product.  Exported/imported keys stay canonical.
+static void evk_make_mont(he_evk_t *evk)
+{
+  const size_t words = ((size_t)evk->npoly * evk->cap) << G.logn;
+  uint64_t *m = (uint64_t *)(uintptr_t)evk->reserved;
+  if (!m)
+    m = (uint64_t *)pool_alloc(words * 8);
+  k_to_mont(m, evk->data, evk->npoly * evk->cap);
+  evk->reserved = (uint64_t)(uintptr_t)m;
+}
+
+extern "C" void he_free_evk(he_evk_t *evk)
+{
+  if (evk->reserved && G.init)
+    pool_free((void *)(uintptr_t)evk->reserved);
+  obj_free(evk);
+}
 
 extern "C" size_t he_export(const void *vo, uint64_t *host)
 {
@@ -490,6 +507,8 @@ extern "C" void he_import(void *vo, const uint64_t *host, unsigned int nlimbs, d
   o->nlimbs = nlimbs;
   o->scale = scale;
   o->flags = flags;
+  if (o->dnum && o->npoly == 2 * o->dnum && o->cap == G.nmod)
+    evk_make_mont((he_evk_t *)o);  // key objects keep their Montgomery shadow in sync
 }
 
 extern "C" void he_evk_meta(const he_evk_t *evk, uint32_t *galois, uint32_t *dnum)
@@ -519,7 +538,7 @@ extern "C" void he_keypair(he_pk_t *pk, poly_mpi_t *sk)
 static void gen_evk(he_evk_t *evk, const uint64_t *sprime, const poly_mpi_t *sk, uint32_t galois)
 {
   if (evk->data)
-    obj_free(evk);
+    he_free_evk(evk);
   obj_alloc(evk, 2 * G.dnum, G.nmod);
   evk->nlimbs = G.nmod;
   evk->galois = galois;
@@ -534,6 +553,7 @@ static void gen_evk(he_evk_t *evk, const uint64_t *sprime, const poly_mpi_t *sk,
     const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, G.L);
     k_evk_combine(limb(evk, 2 * j, 0), limb(evk, 2 * j + 1, 0), e.p, sk->data, sprime, lo, hi);
   }
+  evk_make_mont(evk);
 }
 
 static uint64_t galois_of_rot(unsigned r)
@@ -763,13 +783,18 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
                acc_stride = 2 * nm * n;
   Ws d01(count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
   k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
-  k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
-  k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
-  unsigned mods[GPQHE_MAXMOD];
-  basis_qp(lvl, mods);
-  k_ntt(limbset(D.p, mods, nm, count * ndig, nm * n), false);
-  k_ks_inner(acc.p, D.p, count, D_stride, acc_stride, rlk->data, lvl, 1, d01.p, d01.p + lvl * n, d01_stride,
-             nullptr, false);
+  if (k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED")) {
+    Ws y(count * d2_stride);
+    k_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl);
+  } else {
+    k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
+    k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
+    unsigned mods[GPQHE_MAXMOD];
+    basis_qp(lvl, mods);
+    k_ntt(limbset(D.p, mods, nm, count * ndig, nm * n), false);
+    k_ks_inner(acc.p, D.p, count, D_stride, acc_stride, rlk->data, lvl, 1, d01.p, d01.p + lvl * n, d01_stride,
+               nullptr, false);
+  }
   k_moddown(out, out_pstride, acc.p, nm * n, 2 * count, lvl, rescale ? 1 : 0);
 }
 
@@ -942,7 +967,7 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
     gpqhe_die("he_mul_rescale_batch: bad level %u", lvl);
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  const size_t per_ct = (size_t)(2 * lvl + lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
+  const size_t per_ct = (size_t)(2 * lvl + 2 * lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
   const size_t budget = (size_t)2 << 30;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));

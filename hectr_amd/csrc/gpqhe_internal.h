@@ -263,5 +263,9 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t seed);
 void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
+bool k_ks_fused_ok();
+void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
+                       const uint64_t *evkm, unsigned count, unsigned lvl);
+void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();
 void tables_free();

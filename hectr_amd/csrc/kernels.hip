@@ -38,12 +38,12 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 // ===========================================================================
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
-  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_COUNT
+  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_COUNT
 };
 static const char *kc_names[KC_COUNT] = {
   "ntt_whole_kernel<false>", "ntt_whole_kernel<true>", "ntt_cols_kernel<false>", "ntt_rows_kernel<false>",
   "ntt_rows_kernel<true>", "ntt_cols_kernel<true>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
-  "down_conv_kernel", "down_combine_kernel"};
+  "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -455,6 +455,14 @@ __device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_
   }
 }
 
+// Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
+// B reads 16 consecutive columns per thread at a 16-column lane stride; the
+// XOR spreads those lanes over distinct banks (8-way conflict without it).
+__device__ __forceinline__ int rswz(int c)
+{
+  return c ^ ((c >> 4) & 15);
+}
+
 // block -> (limb, tile) in prime-major order: all tiles of all limbs that use
 // basis slot t run before slot t + 1.
 __device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsigned &v, unsigned &tile)
@@ -470,7 +478,8 @@ __device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsi
 
 // Column pass: tile = T rows x C columns (T C = 4096).
 template <int LOGT, bool INV>
-__global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, unsigned logn, Tw2 tw, const ModConst *mcs)
+__global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+                                                         const ModConst *mcs, const uint64_t *post)
 {
   constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
@@ -480,7 +489,8 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, unsigned logn
   const unsigned m = s.mod(v);
   const ModConst mc = mcs[m];
   const uint64_t q = mc.q, q2 = 2 * q;
-  uint64_t *x = s.limb(v, logn) + (size_t)tile * C;
+  const uint64_t *x = s.limb(v, logn) + (size_t)tile * C;
+  uint64_t *y = o.limb(v, logn) + (size_t)tile * C;
   const int t = threadIdx.x;
   if constexpr (!INV) {
     const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
@@ -508,7 +518,7 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, unsigned logn
       fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        x[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+        y[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
     }
   } else {
     const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
@@ -532,16 +542,20 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, unsigned logn
       for (int k = 0; k < EA; k++)
         r[k] = lds[(l + 16 * k) * CP + c];
       inv_stages<LEA>(r, tw2, T, 4, q);
+      // final scale: n^-1, or a caller constant per limb slot (e.g. n^-1 times
+      // the ModUp factor [(Q_j/q_i)^-1]_{q_i}, folded into the INTT)
+      const uint64_t sw = post ? post[2 * (v % s.per)] : mc.ninv, swp = post ? post[2 * (v % s.per) + 1] : mc.ninvp;
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        x[(size_t)(l + 16 * k) * n2 + c] = mul_shoup(r[k], mc.ninv, mc.ninvp, q);
+        y[(size_t)(l + 16 * k) * n2 + c] = mul_shoup(r[k], sw, swp, q);
     }
   }
 }
 
 // Row pass: tile = R rows x N2 columns (R N2 = 4096).
 template <int LOGN2, bool INV>
-__global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn, Tw2 tw, const ModConst *mcs)
+__global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+                                                         const ModConst *mcs)
 {
   constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
@@ -552,7 +566,8 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn
   const ModConst mc = mcs[m];
   const uint64_t q = mc.q, q2 = 2 * q;
   const unsigned row0 = tile * R;
-  uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
+  const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
+  uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
   const int t = threadIdx.x;
   if constexpr (!INV) {
     const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
@@ -566,7 +581,7 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn
       fwd_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, LOGN2 - 1, q);
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        lds[rr * SP + l + 16 * k] = r[k];
+        lds[rr * SP + rswz(l + 16 * k)] = r[k];
     }
     __syncthreads();
     {
@@ -574,24 +589,24 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn
       uint64_t r[16];
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        r[k] = lds[rr * SP + 16 * g + k];
+        r[k] = lds[rr * SP + rswz(16 * g + k)];
       fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        lds[rr * SP + 16 * g + k] = canon4(r[k], q, q2);
+        lds[rr * SP + rswz(16 * g + k)] = canon4(r[k], q, q2);
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int e = t + 256 * i;
-      x[e] = lds[(e >> LOGN2) * SP + (e & (N2 - 1))];
+      y[e] = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
     }
   } else {
     const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int e = t + 256 * i;
-      lds[(e >> LOGN2) * SP + (e & (N2 - 1))] = x[e];
+      lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = x[e];
     }
     __syncthreads();
     {
@@ -599,11 +614,11 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn
       uint64_t r[16];
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        r[k] = lds[rr * SP + 16 * g + k];
+        r[k] = lds[rr * SP + rswz(16 * g + k)];
       inv_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        lds[rr * SP + 16 * g + k] = r[k];
+        lds[rr * SP + rswz(16 * g + k)] = r[k];
     }
     __syncthreads();
 #pragma unroll
@@ -612,17 +627,17 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, unsigned logn
       uint64_t r[EA];
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        r[k] = lds[rr * SP + l + 16 * k];
+        r[k] = lds[rr * SP + rswz(l + 16 * k)];
       inv_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, 4, q);
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        x[(rr << LOGN2) + l + 16 * k] = canon4(r[k], q, q2);
+        y[(rr << LOGN2) + l + 16 * k] = canon4(r[k], q, q2);
     }
   }
 }
 
 template <int LOGT1, int LOGN2>
-static void ntt2_launch(const LimbSet &s, bool inverse)
+static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const uint64_t *post)
 {
   const unsigned logn = G.logn, n = G.n;
   const unsigned blocks = s.count * (n / 4096);
@@ -631,23 +646,44 @@ static void ntt2_launch(const LimbSet &s, bool inverse)
   if (!inverse) {
     {
       ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
-      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
-                         G.dev.mc);
+      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
+                         G.dev.mc, (const uint64_t *)nullptr);
     }
     ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
-    hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+    hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
                        G.dev.mc);
   } else {
     {
       ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
-      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
+      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
                          G.dev.mc);
     }
     ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
-    hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, s, logn, tw,
-                       G.dev.mc);
+    hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
+                       G.dev.mc, post);
   }
   HIP_CHECK(hipGetLastError());
+}
+
+// v2 path available for this ring degree?
+static bool ntt2_ok()
+{
+  return G.logn >= 13 && G.logn <= 16 && !getenv("GPQHE_NTT_V1");
+}
+
+// Out-of-place NTT (in and out have the same geometry; out may equal in);
+// `post` (inverse only) replaces n^-1 by per-slot Shoup pairs post[2 (v % per)].
+void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_t *post)
+{
+  if (!in.count)
+    return;
+  switch (G.logn) {
+  case 13: ntt2_launch<6, 7>(in, out, inverse, post); return;
+  case 14: ntt2_launch<7, 7>(in, out, inverse, post); return;
+  case 15: ntt2_launch<7, 8>(in, out, inverse, post); return;
+  case 16: ntt2_launch<8, 8>(in, out, inverse, post); return;
+  default: gpqhe_die("k_ntt_ex: ring degree 2^%u not supported", G.logn);
+  }
 }
 
 void k_ntt(const LimbSet &s, bool inverse)
@@ -666,14 +702,9 @@ void k_ntt(const LimbSet &s, bool inverse)
     HIP_CHECK(hipGetLastError());
     return;
   }
-  if (!getenv("GPQHE_NTT_V1")) {
-    switch (logn) {
-    case 13: ntt2_launch<6, 7>(s, inverse); return;
-    case 14: ntt2_launch<7, 7>(s, inverse); return;
-    case 15: ntt2_launch<7, 8>(s, inverse); return;
-    case 16: ntt2_launch<8, 8>(s, inverse); return;
-    default: break;
-    }
+  if (ntt2_ok()) {
+    k_ntt_ex(s, s, inverse, nullptr);
+    return;
   }
   const unsigned logn1 = logn / 2;  // 13:6x7 14:7x7 15:7x8 16:8x8 17:8x9
   const unsigned logn2 = logn - logn1;
@@ -1045,7 +1076,8 @@ static unsigned basis_qp(unsigned lvl, unsigned *mods)
 
 struct UpTable {
   UpDigit *dig;   // [ndig]
-  uint64_t *c;    // [ndig][8][nm]
+  uint64_t *c;    // [ndig][8][nm]  [Qj/q_i]_t 2^64 mod q_t (Montgomery form)
+  uint64_t *ysc;  // [lvl][2]       n^-1 [(Qj/q_i)^-1]_{q_i} + Shoup (folded into the INTT)
   unsigned ndig, nm;
 };
 
@@ -1084,9 +1116,18 @@ static UpTable &up_table(unsigned lvl)
       }
     }
   }
+  std::vector<uint64_t> ysc(2 * (size_t)lvl);
+  for (unsigned i = 0; i < lvl; i++) {
+    const UpDigit &d = dig[i / G.alpha];
+    const uint64_t w = hm_mul_mod(G.mc[i].ninv, d.y[i - d.lo], G.q[i]);
+    ysc[2 * i] = w;
+    ysc[2 * i + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[i]);
+  }
   UpTable tab;
   tab.ndig = ndig;
   tab.nm = nm;
+  HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.dig, ndig * sizeof(UpDigit)));
   HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
   HIP_CHECK(hipMemcpy(tab.dig, dig.data(), ndig * sizeof(UpDigit), hipMemcpyHostToDevice));
@@ -1215,6 +1256,324 @@ void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_strid
   hipLaunchKernelGGL(ks_inner_kernel, dim3((G.n + TPB - 1) / TPB, count, nm), dim3(TPB), 0, G.stream, acc, D,
                      G.logn, lvl, G.L, nm, G.nmod, ndig, d_stride, acc_stride, evk, g, c0, c1, c_stride,
                      (size_t)0, pt, accumulate ? 1 : 0, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+
+// ===========================================================================
+// Fused key switching for ciphertext batches (n = 2^13 .. 2^16).
+//
+//   y      = INTT(d2) with n^-1 (Qj/q_i)^-1 folded into the last pass
+//   T1     = forward column pass of FBC_{j->t}(y)  (ks_cols_kernel; the
+//            converted digit never reaches HBM)
+//   acc    = sum_j NTTrows(T1[j][t]) evk_j[t] + P (d0, d1)   (ks_rows_kernel;
+//            own-digit limbs come straight from the NTT-form d2)
+// Block orders: ks_cols walks the targets fastest (a digit's y tile is reused
+// from L2 by all its targets); ks_rows walks ciphertexts fastest and basis
+// slots slowest (each evk tile and twiddle table is read from HBM once per
+// chunk).
+// ===========================================================================
+
+// XCD-aware grouping: workgroups are dealt round-robin over the 8 XCDs, so
+// blocks b and b + 8 share one XCD's L2.  Map block b to (group g, member i)
+// such that the `members` blocks of a group share b % 8 and are dispatched
+// close together; groups are padded to a multiple of 8 (extra blocks exit).
+// Placement only affects speed, never correctness.
+__device__ __forceinline__ bool xcd_group(unsigned members, unsigned ngroups, unsigned &g, unsigned &i)
+{
+  const unsigned b = blockIdx.x, x = b & 7, s = b >> 3;
+  i = s % members;
+  g = (s / members) * 8 + x;
+  return g < ngroups;
+}
+
+static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
+{
+  return ((ngroups + 7) / 8) * 8 * members;
+}
+
+template <int LOGT>
+__global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
+                                                       size_t t1_stride, unsigned logn, unsigned lvl, unsigned L,
+                                                       unsigned nm, unsigned ndig, unsigned ngroups, UpTable tab,
+                                                       Tw2 tw, const ModConst *mcs)
+{
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
+  const unsigned n2 = 1u << (logn - LOGT);
+  const unsigned tiles = n2 / C;
+  unsigned grp, t;  // group = (p, j, tile) on one XCD; members = basis targets
+  if (!xcd_group(nm, ngroups, grp, t))
+    return;
+  const unsigned tile = grp % tiles, pj = grp / tiles, p = pj / ndig, j = pj % ndig;
+  const UpDigit *dg = tab.dig + j;
+  const unsigned lo = dg->lo, na = dg->na;
+  if (t >= lo && t < lo + na)
+    return;  // own limb: the row pass reads it from the NTT-form d2
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const uint64_t *yb = ybuf + p * y_stride + ((size_t)lo << logn) + (size_t)tile * C;
+  uint64_t cc[8];
+#pragma unroll
+  for (unsigned i = 0; i < 8; i++)
+    cc[i] = i < na ? tab.c[((size_t)j * 8 + i) * nm + t] : 0;
+  uint64_t *out = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + (size_t)tile * C;
+  const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+  const int th = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < C / 16; it++) {
+    const int item = th + 256 * it, c = item % C, l = item / C;
+    uint64_t r[EA];
+#pragma unroll
+    for (int k = 0; k < EA; k++) {
+      const size_t idx = (size_t)(l + 16 * k) * n2 + c;
+      unsigned __int128 acc = 0;
+#pragma unroll
+      for (unsigned i = 0; i < 8; i++)
+        if (i < na)
+          acc += (unsigned __int128)yb[((size_t)i << logn) + idx] * cc[i];
+      r[k] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc);
+    }
+    fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
+#pragma unroll
+    for (int k = 0; k < EA; k++)
+      lds[(l + 16 * k) * CP + c] = r[k];
+  }
+  __syncthreads();
+  {
+    const int c = th % C, g = th / C;
+    uint64_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = lds[(16 * g + k) * CP + c];
+    fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+  }
+}
+
+// Key layout used by ks_rows: inside every 4096-element row tile (R rows x N2),
+// element rr N2 + 16 g + k sits at k 256 + rr (N2 / 16) + g, i.e. in the
+// register ownership of round B, so every thread's 16 key words are loaded
+// coalesced.
+__device__ __forceinline__ unsigned own_perm(unsigned idx, unsigned logn2)
+{
+  const unsigned tile = idx >> 12, e = idx & 4095;
+  const unsigned rr = e >> logn2, c = e & ((1u << logn2) - 1), g = c >> 4, k = c & 15;
+  const unsigned th = (rr << (logn2 - 4)) + g;
+  return (tile << 12) + (k << 8) + th;
+}
+
+template <int LOGN2>
+__global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
+                                                       size_t d2_stride, const uint64_t *d01, size_t d01_stride,
+                                                       const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
+                                                       unsigned logn, unsigned lvl, unsigned L, unsigned nm,
+                                                       unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
+                                                       Tw2 tw, const ModConst *mcs)
+{
+  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
+  __shared__ uint64_t acc1[16 * 256];  // a1 accumulators, thread-private slots k 256 + th
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / R;
+  unsigned grp, p;  // group = (basis slot t, tile) on one XCD; members = ciphertexts
+  if (!xcd_group(count, nm * tiles, grp, p))
+    return;
+  const unsigned t = grp / tiles, tile = grp % tiles;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * R;
+  const size_t toff = (size_t)row0 << LOGN2;  // tile offset inside a limb
+  const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+  const int th = threadIdx.x;
+  const int g = th % (N2 / 16), rr = th / (N2 / 16);
+  // natural-layout tile <-> round-B ownership through the swizzled LDS tile
+  auto load_own = [&](const uint64_t *src, uint64_t (&r)[16]) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int e = th + 256 * i;
+      lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = src[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = lds[rr * SP + rswz(16 * g + k)];
+  };
+  auto store_own = [&](uint64_t *dst, const uint64_t (&r)[16]) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      lds[rr * SP + rswz(16 * g + k)] = r[k];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int e = th + 256 * i;
+      dst[e] = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
+    }
+  };
+  // 64-bit lazy accumulators in [0, 2q): each product v * evk_mont is reduced
+  // by a REDC without its final correction (v, evk < q gives a result < 2q)
+  uint64_t a0[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++)
+    a0[k] = acc1[256 * k + threadIdx.x] = 0;
+  auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
+    const uint64_t lo = v * w, hi = mulhi64(v, w);
+    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
+    a = lazy_lt2q(a + r, q2);
+  };
+  for (unsigned j = 0; j < ndig; j++) {
+    const uint64_t *eb = evkm + (((size_t)(2 * j) * nmod + m) << logn) + toff + th;
+    const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
+    uint64_t r[16];
+    if (t < lvl && t / alpha == j) {
+      load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, r);  // own digit: NTT-form d2
+    } else {
+      const uint64_t *x = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < R / 16; it++) {
+        const int item = th + 256 * it, l = item % 16, ra = item / 16;
+        uint64_t v[EA];
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          v[k] = x[(ra << LOGN2) + l + 16 * k];
+        fwd_stages<LEA>(v, tw2, (uint64_t)(n1 + row0 + ra) << LOGN2, LOGN2 - 1, q);
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          lds[ra * SP + rswz(l + 16 * k)] = v[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = lds[rr * SP + rswz(16 * g + k)];
+      fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = canon4(r[k], q, q2);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      mac(a0[k], r[k], eb[256 * k]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      uint64_t a = acc1[256 * k + th];
+      mac(a, r[k], ea[256 * k]);
+      acc1[256 * k + th] = a;
+    }
+  }
+  uint64_t a1[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+    a1[k] = acc1[256 * k + th];
+    a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+  }
+  if (t < lvl) {
+    uint64_t c[16];
+    const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
+    load_own(c0, c);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      a0[k] = add_mod(a0[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
+    load_own(c0 + ((size_t)lvl << logn), c);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      a1[k] = add_mod(a1[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
+  }
+  uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
+  store_own(o0, a0);
+  store_own(o0 + ((size_t)nm << logn), a1);
+}
+
+template <int LOGT1, int LOGN2>
+static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
+                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl)
+{
+  UpTable &tab = up_table(lvl);
+  const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
+  const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
+               d01_stride = 2 * (size_t)lvl * n, acc_stride = 2 * (size_t)nm * n;
+  const Tw2 tw{G.tw2, G.itw2};
+  const unsigned tiles = n / 4096;
+  const double own = (double)G.alpha * ndig;  // digit slots not converted (approx. for partial digits)
+  {
+    // reads the digit's alpha limbs once per target tile set (L2), writes the
+    // converted + column-transformed limb
+    ProfScope ps(KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
+    const unsigned ngroups = tiles * count * ndig;
+    hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y, y_stride,
+                       T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
+  }
+  // reads T1 (+ own d2 limbs, d0/d1) per ciphertext and the key once, writes acc
+  ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2 * lvl + 2 * nm) +
+                                      2.0 * ndig * nm));
+  hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * tiles)), dim3(256), 0, G.stream, T1,
+                     t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
+                     ndig, G.alpha, count, tw, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+bool k_ks_fused_ok()
+{
+  return ntt2_ok() && G.alpha <= 8;
+}
+
+// Fused relinearization core for `count` ciphertexts: d01 [count][2][lvl],
+// d2n [count][lvl] (NTT form), ybuf/T1 workspaces; writes acc [count][2][nm].
+void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
+                       const uint64_t *evkm, unsigned count, unsigned lvl)
+{
+  UpTable &tab = up_table(lvl);
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned i = 0; i < lvl; i++)
+    mods[i] = i;
+  LimbSet in{}, out{};
+  in.base = (uint64_t *)d2n;
+  out.base = ybuf;
+  in.stride = out.stride = (size_t)lvl * G.n;
+  in.per = out.per = lvl;
+  in.count = out.count = lvl * count;
+  for (unsigned i = 0; i < lvl; i++)
+    in.mods[i] = out.mods[i] = (uint8_t)mods[i];
+  k_ntt_ex(in, out, true, tab.ysc);
+  switch (G.logn) {
+  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
+  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
+  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
+  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
+  default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^16");
+  }
+}
+
+// Montgomery-form copy of a key (x 2^64 mod q per limb), used by the fused
+// inner product.
+__global__ void to_mont_kernel(uint64_t *out, const uint64_t *in, unsigned logn, unsigned nmod, unsigned logn2,
+                               const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned limb = blockIdx.y % nmod;
+  const size_t base = (size_t)blockIdx.y << logn;
+  const ModConst m = mc[limb];
+  const size_t dst = logn2 ? own_perm((unsigned)k, logn2) : k;
+  out[base + dst] = mul_mod(in[base + k], m.r64, m);
+}
+
+// Montgomery copy (x 2^64 mod q) of nlimbs_total limbs (limb slot = index %
+// nmod), laid out for ks_rows when the fused path serves this ring degree.
+void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
+{
+  const unsigned logn2 = k_ks_fused_ok() ? (G.logn >= 15 ? 8 : 7) : 0;
+  hipLaunchKernelGGL(to_mont_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs_total), dim3(TPB), 0, G.stream, out, in,
+                     G.logn, G.nmod, logn2, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1460,6 +1819,7 @@ void tables_free()
   for (auto &kv : g_up) {
     HIP_CHECK(hipFree(kv.second.dig));
     HIP_CHECK(hipFree(kv.second.c));
+    HIP_CHECK(hipFree(kv.second.ysc));
   }
   g_up.clear();
   for (auto &kv : g_down) {

@@ -1,0 +1,90 @@
+"""N > 1 path of bench.py on the CPU: two ranks (gloo) shard a global batch of
+ciphertext pairs, each with a replica of the context and relinearization key
+(same seed), multiply their shard with the oracle engine, and rank 0 checks
+that the gathered shards equal a single-process run of the whole batch and
+that the max-over-ranks reduction is what `value` uses."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+PARAMS = dict(logn=10, nlimbs=3, nspecial=1, dnum=3, slots=8, q0_bits=50, qi_bits=40, p_bits=55, seed=77)
+GLOBAL = 7  # pairs (uneven split on purpose)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run_batch(first, count):
+    from hectr_amd import dist
+    from hectr_amd.gpqhe import Engine
+    e = Engine.oracle()
+    e.init_params(**PARAMS)
+    pk, sk, rlk = e.pk(), e.sk(), e.evk()
+    e.keypair(pk, sk)
+    e.genrlk(rlk, sk)
+    L, n = e.L, e.n
+    a = np.zeros(max(count, 1) * 2 * L * n, dtype=np.uint64)
+    b = np.zeros_like(a)
+    out = np.zeros(max(count, 1) * 2 * (L - 1) * n, dtype=np.uint64)
+    dist.fill_pairs(e.lib, a.ctypes.data, b.ctypes.data, first, count, L, n)
+    if count:
+        e.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, count, L, ctypes.byref(rlk))
+    e.exit()
+    return out[:count * 2 * (L - 1) * n]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from hectr_amd import dist
+    try:
+        r, w, _ = dist.init("gloo")
+        first, stop = dist.shard(GLOBAL, r, w)
+        out = _run_batch(first, stop - first)
+        t = dist.max_over_ranks(float(r + 1))
+        parts = dist.gather(out)
+        dist.barrier()
+        if r == 0:
+            q.put((np.concatenate(parts), t))
+        import torch.distributed as td
+        td.destroy_process_group()
+    except Exception as exc:  # pragma: no cover - surfaced to the parent
+        q.put(exc)
+        raise
+
+
+def test_shard_bounds():
+    from hectr_amd.dist import shard
+    for count in (0, 1, 7, 256):
+        for world in (1, 2, 3, 8):
+            spans = [shard(count, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == count
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def test_two_rank_gloo_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+    if isinstance(res, Exception):
+        raise res
+    gathered, tmax = res
+    assert tmax == 2.0
+    single = _run_batch(0, GLOBAL)
+    assert np.array_equal(gathered, single)

@@ -24,6 +24,8 @@ PARAMS = {
     "hyb": ("params", dict(logn=13, nlimbs=5, nspecial=2, dnum=3, slots=32, q0_bits=58, qi_bits=45,
                            p_bits=59)),
     "bench": ("params", dict(logn=16, nlimbs=8, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
+    "bench_d2": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=60, qi_bits=50,
+                                p_bits=60)),
 }
 
 
@@ -141,27 +143,61 @@ def test_ntt_batch_bitexact(oracle, product):
     assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
 
 
-def test_mul_rescale_batch_bitexact(oracle, product):
-    """Config 3 op at n=2^16, L=8 on 3 random-residue ciphertext pairs."""
+@pytest.mark.parametrize("name", ["bench", "bench_d2"])
+def test_mul_rescale_batch_bitexact(oracle, product, name):
+    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4) on 3
+    random-residue ciphertext pairs."""
+    import ctypes
     import torch
-    init_both(oracle, product, "bench")
+    init_both(oracle, product, name)
     n, L, cnt = product.n, product.L, 3
-    for e in (oracle, product):
-        e.set_seed(77)
     _, _, _, rlk_o = keys(oracle, rot=False)
     _, _, _, rlk_p = keys(product, rot=False)
     same(oracle, product, rlk_o, rlk_p)
     words = cnt * 2 * L * n
-    a = np.zeros(words, dtype=np.uint64); b = np.zeros(words, dtype=np.uint64)
+    a = np.zeros(words, dtype=np.uint64)
+    b = np.zeros(words, dtype=np.uint64)
     oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 1)
     oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 2)
     out_o = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
-    import ctypes
     oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk_o))
-    da = torch.from_numpy(a.view(np.int64)).cuda(); db = torch.from_numpy(b.view(np.int64)).cuda()
+    da = torch.from_numpy(a.view(np.int64)).cuda()
+    db = torch.from_numpy(b.view(np.int64)).cuda()
     dout = torch.zeros(out_o.size, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, L, ctypes.byref(rlk_p))
     product.sync()
     got = dout.cpu().numpy().view(np.uint64)
     assert np.array_equal(got, out_o), f"{np.count_nonzero(got != out_o)} residues differ"
+
+
+def test_batch_real_encryptions_decode(product):
+    """a 4-ciphertext subset of real encryptions of
+    uniform reals in [-1, 1] through he_mul_rescale_batch decodes to the
+    slot-wise products (bench parameters, dnum=2/K=4)."""
+    import ctypes
+    import torch
+    kind, kw = PARAMS["bench_d2"]
+    product.init_params(**kw)
+    product.set_seed(9)
+    pk, sk, _, rlk = keys(product, rot=False)
+    n, L, s, cnt = product.n, product.L, product.slots, 4
+    rng = np.random.default_rng(12)
+    za = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
+    zb = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
+    ha = np.concatenate([product.export(product.encrypt(z, pk)).ravel() for z in za])
+    hb = np.concatenate([product.export(product.encrypt(z, pk)).ravel() for z in zb])
+    da = torch.from_numpy(ha.view(np.int64)).cuda()
+    db = torch.from_numpy(hb.view(np.int64)).cuda()
+    dout = torch.zeros(cnt * 2 * (L - 1) * n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, L, ctypes.byref(rlk))
+    product.sync()
+    out = dout.cpu().numpy().view(np.uint64).reshape(cnt, -1)
+    delta = product.info.delta
+    for i in range(cnt):
+        ct = product.ct()
+        product.import_(ct, out[i], L - 1, scale=delta * delta / product.primes[L - 1])
+        got = product.decrypt(ct, sk)
+        assert np.abs(got - za[i] * zb[i]).max() < 1e-6
+        product.free(ct)
