@@ -1354,6 +1354,87 @@ __global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size
   }
 }
 
+// Multi-target variant for digits of at most 4 limbs: the block loads its
+// (p, j, tile) digit values into registers once and converts them for NT
+// targets in turn (the single-target kernel re-reads them through L2 for every
+// target and waits on those loads most of its time).  Column tiles are double
+// buffered in LDS, so one barrier per target suffices.
+template <int LOGT, int NT>
+__global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
+                                                           size_t t1_stride, unsigned logn, unsigned lvl,
+                                                           unsigned L, unsigned nm, unsigned ndig, unsigned members,
+                                                           unsigned ngroups, UpTable tab, Tw2 tw,
+                                                           const ModConst *mcs)
+{
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2][T * CP];
+  const unsigned n2 = 1u << (logn - LOGT);
+  const unsigned tiles = n2 / C;
+  unsigned grp, mi;  // group = (p, j, tile) on one XCD; members = target batches
+  if (!xcd_group(members, ngroups, grp, mi))
+    return;
+  const unsigned tile = grp % tiles, pj = grp / tiles, p = pj / ndig, j = pj % ndig;
+  const UpDigit *dg = tab.dig + j;
+  const unsigned lo = dg->lo, na = dg->na;
+  if (mi * NT >= nm - na)
+    return;
+  const uint64_t *yb = ybuf + p * y_stride + ((size_t)lo << logn) + (size_t)tile * C;
+  const int th = threadIdx.x;
+  uint64_t y[IT][4][EA];
+#pragma unroll
+  for (int it = 0; it < IT; it++) {
+    const int item = th + 256 * it, c = item % C, l = item / C;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        y[it][i][k] = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+  }
+  for (int u = 0; u < NT; u++) {
+    const unsigned ui = mi * NT + u;
+    if (ui >= nm - na)
+      break;
+    const unsigned t = ui < lo ? ui : ui + na;  // skip the digit's own limbs
+    const unsigned m = basis_mod(t, lvl, L);
+    const ModConst mc = mcs[m];
+    const uint64_t q = mc.q, q2 = 2 * q;
+    uint64_t cc[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      cc[i] = i < (int)na ? tab.c[((size_t)j * 8 + i) * nm + t] : 0;
+    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+    uint64_t *buf = lds[u & 1];
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int item = th + 256 * it, c = item % C, l = item / C;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++) {
+        unsigned __int128 acc = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          acc += (unsigned __int128)y[it][i][k] * cc[i];
+        r[k] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc);
+      }
+      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        buf[(l + 16 * k) * CP + c] = r[k];
+    }
+    __syncthreads();
+    uint64_t *out = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + (size_t)tile * C;
+    const int c = th % C, g = th / C;
+    uint64_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = buf[(16 * g + k) * CP + c];
+    fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+  }
+}
+
 // Key layout used by ks_rows: inside every 4096-element row tile (R rows x N2),
 // element rr N2 + 16 g + k sits at k 256 + rr (N2 / 16) + g, i.e. in the
 // register ownership of round B, so every thread's 16 key words are loaded
@@ -1507,8 +1588,17 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     // converted + column-transformed limb
     ProfScope ps(KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
     const unsigned ngroups = tiles * count * ndig;
-    hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y, y_stride,
-                       T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
+    if (G.alpha <= 4 && !getenv("GPQHE_KSCOLS1")) {
+      constexpr unsigned NT = 4;
+      const unsigned na_min = lvl - (ndig - 1) * G.alpha;  // the last digit may be partial
+      const unsigned members = (nm - na_min + NT - 1) / NT;
+      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream,
+                         y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw,
+                         G.dev.mc);
+    } else {
+      hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
+                         y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
+    }
   }
   // reads T1 (+ own d2 limbs, d0/d1) per ciphertext and the key once, writes acc
   ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2 * lvl + 2 * nm) +
