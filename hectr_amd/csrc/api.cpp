@@ -785,7 +785,14 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
   k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
   if (k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED")) {
     Ws y(count * d2_stride);
-    k_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl);
+    const int mode = rescale ? 1 : 0;
+    const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
+    k_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl,
+                      dn_fused ? (rescale ? lvl - 1 : lvl) : 0);
+    if (dn_fused) {
+      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, d01.p, lvl * n);
+      return;
+    }
   } else {
     k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
     k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);

@@ -38,12 +38,14 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 // ===========================================================================
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
-  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_COUNT
+  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
+  KC_DN_ROWS, KC_COUNT
 };
 static const char *kc_names[KC_COUNT] = {
   "ntt_whole_kernel<false>", "ntt_whole_kernel<true>", "ntt_cols_kernel<false>", "ntt_rows_kernel<false>",
   "ntt_rows_kernel<true>", "ntt_cols_kernel<true>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
-  "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel"};
+  "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
+  "dn_rows_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -1453,7 +1455,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                        unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
-                                                       Tw2 tw, const ModConst *mcs)
+                                                       unsigned p_lo, Tw2 tw, const ModConst *mcs)
 {
   constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
@@ -1555,7 +1557,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
     a1[k] = acc1[256 * k + th];
     a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
   }
-  if (t < lvl) {
+  if (t < lvl && t >= p_lo) {
     uint64_t c[16];
     const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
     load_own(c0, c);
@@ -1574,7 +1576,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
 
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
-                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl)
+                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo)
 {
   UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
@@ -1601,23 +1603,23 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     }
   }
   // reads T1 (+ own d2 limbs, d0/d1) per ciphertext and the key once, writes acc
-  ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2 * lvl + 2 * nm) +
-                                      2.0 * ndig * nm));
+  ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
+                                                       2 * nm) + 2.0 * ndig * nm));
   hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * tiles)), dim3(256), 0, G.stream, T1,
                      t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
-                     ndig, G.alpha, count, tw, G.dev.mc);
+                     ndig, G.alpha, count, p_lo, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
 bool k_ks_fused_ok()
 {
-  return ntt2_ok() && G.alpha <= 8;
+  return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
 }
 
 // Fused relinearization core for `count` ciphertexts: d01 [count][2][lvl],
 // d2n [count][lvl] (NTT form), ybuf/T1 workspaces; writes acc [count][2][nm].
 void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
-                       const uint64_t *evkm, unsigned count, unsigned lvl)
+                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo)
 {
   UpTable &tab = up_table(lvl);
   unsigned mods[GPQHE_MAXMOD];
@@ -1633,10 +1635,10 @@ void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, 
     in.mods[i] = out.mods[i] = (uint8_t)mods[i];
   k_ntt_ex(in, out, true, tab.ysc);
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
-  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
-  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
-  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl); break;
+  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
+  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
+  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
+  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^16");
   }
 }
@@ -1670,6 +1672,8 @@ void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
 // ModDown table: divide by the product of the drop moduli (basis positions
 // [keep, nm)), keep basis positions [0, keep).
 struct DownTable {
+  uint64_t *ysc;     // [nd][2]     n^-1 [(Dprod/d)^-1]_d + Shoup (folded into the INTT)
+  uint64_t *fin;     // [keep][2]   factor of the d0/d1 term added after division (+ Shoup)
   uint64_t *y, *yp;  // [nd]        [(Dprod/d)^-1]_d
   uint64_t *c;       // [nd][keep]  [Dprod/d]_t
   uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
@@ -1719,9 +1723,28 @@ static DownTable &down_table(unsigned lvl, int mode)
     dinv[t] = hm_inv_mod(dp, qt);
     dinvp[t] = (uint64_t)(((unsigned __int128)dinv[t] << 64) / qt);
   }
+  // fused ModDown: d0/d1 enter after division by Dprod; P Dprod^-1 is 1 (mode
+  // 0) or q_{lvl-1}^-1 (mode 1)
+  std::vector<uint64_t> ysc(2 * (size_t)nd), fin(2 * (size_t)keep);
+  for (unsigned d = 0; d < nd; d++) {
+    const unsigned md = mods[keep + d];
+    const uint64_t w = hm_mul_mod(G.mc[md].ninv, y[d], G.q[md]);
+    ysc[2 * d] = w;
+    ysc[2 * d + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[md]);
+  }
+  for (unsigned t = 0; t < keep; t++) {
+    const uint64_t qt = G.q[mods[t]];
+    const uint64_t f = mode == 1 ? hm_inv_mod(G.q[lvl - 1] % qt, qt) : 1 % qt;
+    fin[2 * t] = f;
+    fin[2 * t + 1] = (uint64_t)(((unsigned __int128)f << 64) / qt);
+  }
   DownTable tab;
   tab.keep = keep;
   tab.nd = nd;
+  HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
+  HIP_CHECK(hipMalloc(&tab.fin, fin.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(tab.fin, fin.data(), fin.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.y, nd * 8));
   HIP_CHECK(hipMalloc(&tab.yp, nd * 8));
   HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
@@ -1822,6 +1845,214 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
   pool_free(conv);
 }
 
+// ===========================================================================
+// Fused ModDown for ciphertext batches (mode 0 / 1, n = 2^13 .. 2^16).
+//
+//   Y    = INTT(X drop limbs) with n^-1 [(Dprod/d)^-1]_d folded into the last
+//          pass (in place)
+//   conv = forward column pass of FBC_{drop->t}(Y)      (dn_cols_kernel)
+//   out  = (X_t - NTTrows(conv_t)) Dprod^-1 + fin_t d01_t  (dn_rows_kernel)
+// The converted polynomial never reaches HBM in coefficient form and the
+// combine is the row pass's epilogue.
+// ===========================================================================
+template <int LOGT, int NT, bool X5>
+__global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, uint64_t *conv,
+                                                          unsigned logn, unsigned lvl, unsigned L, unsigned members,
+                                                          unsigned ngroups, DownTable tab, Tw2 tw,
+                                                          const ModConst *mcs)
+{
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
+  // fifth drop limb (mode 1 with K = 4), thread-private slots (it EA + k) 256 + th
+  __shared__ uint64_t y5[X5 ? 4096 : 1];
+  const unsigned n2 = 1u << (logn - LOGT);
+  const unsigned tiles = n2 / C;
+  unsigned grp, mi;  // group = (poly, tile) on one XCD; members = target batches
+  if (!xcd_group(members, ngroups, grp, mi))
+    return;
+  const unsigned tile = grp % tiles, p = grp / tiles;
+  const unsigned keep = tab.keep, nd = tab.nd;
+  if (mi * NT >= keep)
+    return;
+  const uint64_t *yb = X + p * x_pstride + ((size_t)keep << logn) + (size_t)tile * C;
+  const int th = threadIdx.x;
+  uint64_t y[IT][4][EA];  // drop limbs 0..3 in registers
+#pragma unroll
+  for (int it = 0; it < IT; it++) {
+    const int item = th + 256 * it, c = item % C, l = item / C;
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        y[it][d][k] = d < (int)nd ? yb[((size_t)d << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+    if constexpr (X5) {
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        y5[(it * EA + k) * 256 + th] = yb[((size_t)4 << logn) + (size_t)(l + 16 * k) * n2 + c];
+    }
+  }
+  for (int u = 0; u < NT; u++) {
+    const unsigned t = mi * NT + u;
+    if (t >= keep)
+      break;
+    const unsigned m = basis_mod(t, lvl, L);
+    const ModConst mc = mcs[m];
+    const uint64_t q = mc.q, q2 = 2 * q;
+    uint64_t cc[5];
+#pragma unroll
+    for (int d = 0; d < 5; d++)
+      cc[d] = d < (int)nd ? tab.c[(size_t)d * keep + t] : 0;
+    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+    if (u)
+      __syncthreads();  // the previous target's round B has read the tile
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int item = th + 256 * it, c = item % C, l = item / C;
+      uint64_t r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++) {
+        unsigned __int128 acc = 0;
+#pragma unroll
+        for (int d = 0; d < 4; d++)
+          acc += (unsigned __int128)y[it][d][k] * cc[d];
+        if constexpr (X5)
+          acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
+        r[k] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc);
+      }
+      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        lds[(l + 16 * k) * CP + c] = r[k];
+    }
+    __syncthreads();
+    uint64_t *out = conv + (((size_t)p * keep + t) << logn) + (size_t)tile * C;
+    const int c = th % C, g = th / C;
+    uint64_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = lds[(16 * g + k) * CP + c];
+    fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+  }
+}
+
+template <int LOGN2>
+__global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint64_t *out, size_t out_pstride,
+                                                       const uint64_t *X, size_t x_pstride, const uint64_t *d01,
+                                                       size_t d01_pstride, unsigned logn, unsigned lvl, unsigned L,
+                                                       unsigned npoly, DownTable tab, Tw2 tw, const ModConst *mcs)
+{
+  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / R;
+  const unsigned keep = tab.keep;
+  unsigned grp, p;  // group = (target t, tile) on one XCD; members = polynomials
+  if (!xcd_group(npoly, keep * tiles, grp, p))
+    return;
+  const unsigned t = grp / tiles, tile = grp % tiles;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * R;
+  const size_t toff = ((size_t)t << logn) + ((size_t)row0 << LOGN2);
+  const uint64_t *x = conv + (((size_t)p * keep) << logn) + toff;
+  const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
+  const int th = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < R / 16; it++) {
+    const int item = th + 256 * it, l = item % 16, rr = item / 16;
+    uint64_t r[EA];
+#pragma unroll
+    for (int k = 0; k < EA; k++)
+      r[k] = x[(rr << LOGN2) + l + 16 * k];
+    fwd_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, LOGN2 - 1, q);
+#pragma unroll
+    for (int k = 0; k < EA; k++)
+      lds[rr * SP + rswz(l + 16 * k)] = r[k];
+  }
+  __syncthreads();
+  {
+    const int g = th % (N2 / 16), rr = th / (N2 / 16);
+    uint64_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = lds[rr * SP + rswz(16 * g + k)];
+    fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      lds[rr * SP + rswz(16 * g + k)] = canon4(r[k], q, q2);
+  }
+  __syncthreads();
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], f = tab.fin[2 * t], fp = tab.fin[2 * t + 1];
+  const uint64_t *xs = X + p * x_pstride + toff;
+  const uint64_t *ds = d01 + p * d01_pstride + toff;
+  uint64_t *o = out + p * out_pstride + toff;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int e = th + 256 * i;
+    const uint64_t cv = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
+    const uint64_t v = mul_shoup(sub_mod(xs[e], cv, q), dinv, dinvp, q);
+    o[e] = add_mod(v, mul_shoup(ds[e], f, fp, q), q);
+  }
+}
+
+template <int LOGT1, int LOGN2>
+static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
+                            const uint64_t *d01, size_t d01_pstride, unsigned npoly, unsigned lvl, DownTable &tab)
+{
+  const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
+  const Tw2 tw{G.tw2, G.itw2};
+  {
+    // reads the nd drop limbs, writes keep column-transformed limbs
+    ProfScope ps(KC_DN_COLS, 8.0 * n * npoly * (tab.nd + keep));
+    constexpr unsigned NT = 4;
+    const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
+    if (tab.nd <= 4)
+      hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
+                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+    else
+      hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
+                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+  }
+  // reads conv, X and d01 keep limbs, writes out
+  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
+  hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * tiles)), dim3(256), 0, G.stream, conv,
+                     out, out_pstride, X, x_pstride, d01, d01_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
+                     int mode, const uint64_t *d01, size_t d01_pstride)
+{
+  if (mode != 0 && mode != 1)
+    gpqhe_die("fused ModDown: mode %d", mode);
+  DownTable &tab = down_table(lvl, mode);
+  if (tab.nd > 5)
+    gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  LimbSet ds{};
+  ds.base = X + ((size_t)tab.keep << G.logn);
+  ds.stride = x_pstride;
+  ds.per = tab.nd;
+  ds.count = tab.nd * npoly;
+  for (unsigned d = 0; d < tab.nd; d++)
+    ds.mods[d] = (uint8_t)mods[tab.keep + d];
+  k_ntt_ex(ds, ds, true, tab.ysc);
+  uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
+  switch (G.logn) {
+  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^16");
+  }
+  pool_free(conv);
+}
+
 // Benchmark input generator (oracle: poly_fill_uniform).
 __global__ void fill_uniform_kernel(uint64_t *data, unsigned logn, unsigned nlimbs, uint64_t seed,
                                     const ModConst *mc)
@@ -1918,6 +2149,8 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.c));
     HIP_CHECK(hipFree(kv.second.dinv));
     HIP_CHECK(hipFree(kv.second.dinvp));
+    HIP_CHECK(hipFree(kv.second.ysc));
+    HIP_CHECK(hipFree(kv.second.fin));
   }
   g_down.clear();
 }
