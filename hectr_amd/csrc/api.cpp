@@ -787,8 +787,9 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
     Ws y(count * d2_stride);
     const int mode = rescale ? 1 : 0;
     const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
+    const unsigned keep = rescale ? lvl - 1 : lvl;
     k_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl,
-                      dn_fused ? (rescale ? lvl - 1 : lvl) : 0);
+                      dn_fused ? keep : 0, dn_fused ? keep : nm);
     if (dn_fused) {
       k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, d01.p, lvl * n);
       return;

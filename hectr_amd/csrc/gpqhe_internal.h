@@ -265,11 +265,13 @@ void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 bool k_ks_fused_ok();
 // p_lo: P (d0, d1) is added to acc limbs t in [p_lo, lvl) only; the fused
-// ModDown adds the remaining d0/d1 terms after its division.
+// ModDown adds the remaining d0/d1 terms after its division.  Limbs t >=
+// drop_lo leave after the inverse row pass (input of k_moddown_fused).
 void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
-                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo);
+                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo);
 // ModDown (mode 0 or 1) of X fused with the d0/d1 terms left out by
-// k_keyswitch_fused(p_lo = mode ? lvl - 1 : lvl); d01 poly p at d01 + p*d01_pstride
+// k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
+// must hold the inverse row pass of their NTT form; d01 poly p at d01 + p*d01_pstride
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
                      unsigned lvl, int mode, const uint64_t *d01, size_t d01_pstride);
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);

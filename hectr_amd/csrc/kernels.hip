@@ -1455,7 +1455,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                        unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
-                                                       unsigned p_lo, Tw2 tw, const ModConst *mcs)
+                                                       unsigned p_lo, unsigned drop_lo, Tw2 tw, const ModConst *mcs)
 {
   constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
@@ -1570,13 +1570,42 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
       a1[k] = add_mod(a1[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
   }
   uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
-  store_own(o0, a0);
-  store_own(o0 + ((size_t)nm << logn), a1);
+  if (t < drop_lo) {
+    store_own(o0, a0);
+    store_own(o0 + ((size_t)nm << logn), a1);
+    return;
+  }
+  // limb dropped by the following ModDown: apply the inverse row pass here (the
+  // registers already hold round B's ownership); dn_cols finishes the INTT
+  const uint64_t *itw2 = tw.inv + ((size_t)m << (logn + 1));
+  auto inv_rows_store = [&](uint64_t *dst, uint64_t (&r)[16]) {
+    inv_stages<4>(r, itw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      lds[rr * SP + rswz(16 * g + k)] = r[k];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < R / 16; it++) {
+      const int item = th + 256 * it, l = item % 16, ra = item / 16;
+      uint64_t v[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        v[k] = lds[ra * SP + rswz(l + 16 * k)];
+      inv_stages<LEA>(v, itw2, (uint64_t)(n1 + row0 + ra) << LOGN2, 4, q);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        dst[(ra << LOGN2) + l + 16 * k] = canon4(v[k], q, q2);
+    }
+  };
+  inv_rows_store(o0, a0);
+  inv_rows_store(o0 + ((size_t)nm << logn), a1);
 }
 
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
-                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo)
+                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
+                            unsigned drop_lo)
 {
   UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
@@ -1607,7 +1636,7 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
                                                        2 * nm) + 2.0 * ndig * nm));
   hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * tiles)), dim3(256), 0, G.stream, T1,
                      t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
-                     ndig, G.alpha, count, p_lo, tw, G.dev.mc);
+                     ndig, G.alpha, count, p_lo, drop_lo, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1619,7 +1648,7 @@ bool k_ks_fused_ok()
 // Fused relinearization core for `count` ciphertexts: d01 [count][2][lvl],
 // d2n [count][lvl] (NTT form), ybuf/T1 workspaces; writes acc [count][2][nm].
 void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
-                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo)
+                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo)
 {
   UpTable &tab = up_table(lvl);
   unsigned mods[GPQHE_MAXMOD];
@@ -1635,10 +1664,10 @@ void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, 
     in.mods[i] = out.mods[i] = (uint8_t)mods[i];
   k_ntt_ex(in, out, true, tab.ysc);
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
-  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
-  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
-  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo); break;
+  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
+  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
+  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
+  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^16");
   }
 }
@@ -1876,21 +1905,59 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
     return;
   const uint64_t *yb = X + p * x_pstride + ((size_t)keep << logn) + (size_t)tile * C;
   const int th = threadIdx.x;
-  uint64_t y[IT][4][EA];  // drop limbs 0..3 in registers
+  // Drop limbs arrive after the inverse row pass (ks_rows); the inverse column
+  // pass with n^-1 [(Dprod/d)^-1]_d runs here.  Limbs 0..3 stay in registers.
+  uint64_t y[IT][4][EA];
 #pragma unroll
-  for (int it = 0; it < IT; it++) {
-    const int item = th + 256 * it, c = item % C, l = item / C;
+  for (int d = 0; d < 5; d++) {
+    if (d >= (int)nd)
+      break;
+    const unsigned md = basis_mod(keep + d, lvl, L);
+    const uint64_t qd = mcs[md].q;
+    const uint64_t *itw2 = tw.inv + ((size_t)md << (logn + 1));
+    const uint64_t w = tab.ysc[2 * d], wp = tab.ysc[2 * d + 1];
+    const uint64_t *src = yb + ((size_t)d << logn);
+    if (d)
+      __syncthreads();
+    {
+      const int c = th % C, g = th / C;
+      uint64_t r[16];
 #pragma unroll
-    for (int d = 0; d < 4; d++)
+      for (int k = 0; k < 16; k++)
+        r[k] = src[(size_t)(16 * g + k) * n2 + c];
+      inv_stages<4>(r, itw2, T + 16 * g, 0, qd);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[(16 * g + k) * CP + c] = r[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IT; it++) {
+      const int item = th + 256 * it, c = item % C, l = item / C;
+      uint64_t r[EA];
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        y[it][d][k] = d < (int)nd ? yb[((size_t)d << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
-    if constexpr (X5) {
+        r[k] = lds[(l + 16 * k) * CP + c];
+      inv_stages<LEA>(r, itw2, T, 4, qd);
 #pragma unroll
-      for (int k = 0; k < EA; k++)
-        y5[(it * EA + k) * 256 + th] = yb[((size_t)4 << logn) + (size_t)(l + 16 * k) * n2 + c];
+      for (int k = 0; k < EA; k++) {
+        const uint64_t v = mul_shoup(r[k], w, wp, qd);
+        if (d < 4)
+          y[it][d < 4 ? d : 0][k] = v;
+        else if constexpr (X5)
+          y5[(it * EA + k) * 256 + th] = v;
+      }
     }
   }
+#pragma unroll
+  for (int d = 0; d < 4; d++)
+    if (d >= (int)nd)
+#pragma unroll
+      for (int it = 0; it < IT; it++)
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          y[it][d][k] = 0;
+  __syncthreads();
   for (int u = 0; u < NT; u++) {
     const unsigned t = mi * NT + u;
     if (t >= keep)
@@ -2006,9 +2073,9 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2};
   {
-    // reads the nd drop limbs, writes keep column-transformed limbs
+    // reads the nd row-transformed drop limbs, writes keep column-transformed limbs
     ProfScope ps(KC_DN_COLS, 8.0 * n * npoly * (tab.nd + keep));
-    constexpr unsigned NT = 4;
+    constexpr unsigned NT = 8;  // one block per (poly, tile): the INTT columns are not recomputed
     const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
     if (tab.nd <= 4)
       hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
@@ -2032,16 +2099,6 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
   DownTable &tab = down_table(lvl, mode);
   if (tab.nd > 5)
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
-  unsigned mods[GPQHE_MAXMOD];
-  basis_qp(lvl, mods);
-  LimbSet ds{};
-  ds.base = X + ((size_t)tab.keep << G.logn);
-  ds.stride = x_pstride;
-  ds.per = tab.nd;
-  ds.count = tab.nd * npoly;
-  for (unsigned d = 0; d < tab.nd; d++)
-    ds.mods[d] = (uint8_t)mods[tab.keep + d];
-  k_ntt_ex(ds, ds, true, tab.ysc);
   uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
   case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
