@@ -132,9 +132,12 @@ def main():
         dom_name = max(stats, key=lambda k: stats[k][1])
         launches, tot_us, nbytes = stats[dom_name]
         achieved = nbytes / tot_us / 1e3  # GB/s
+        workload = (f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, dnum={eng.info.dnum}, "
+                    f"batch={B} pairs per GPU")
+        traffic, src = pmc_traffic(dom_name, workload)
         dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_us": tot_us / launches,
-               "alg_bytes_per_launch": nbytes / launches,
+               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+               "avg_launch_us": tot_us / launches, "alg_bytes_per_launch": nbytes / launches,
                "share_of_step": tot_us / (1e6 * (ti1 - ti0))}
         kernels = {k: {"launches": v[0], "avg_us": v[1] / v[0], "share": v[1] / (1e6 * (ti1 - ti0)),
                        "GBs": v[2] / v[1] / 1e3} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
@@ -151,8 +154,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic random-residue ciphertexts (splitmix64), real relinearization key",
-            "config": {"workload": f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, "
-                                   f"dnum={eng.info.dnum}, batch={B} pairs per GPU",
+            "config": {"workload": workload,
                        "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": K,
                        "dnum": eng.info.dnum, "parallelism": f"batch-sharded x{world}"},
             "event_s_rank0": ev_s,
@@ -174,6 +176,27 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return result
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc.json, written by scripts/prof_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload, with
+    the gfx950 FETCH_SIZE x2 correction).  (None, None) when no profile of this
+    workload exists: PMC counters cannot be read from inside the timed run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime, reverse=True)
+    for f in files:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("meta", {}).get("bench_workload") != workload:
+            continue
+        for name, e in d.get("kernels", {}).items():
+            if (name == kernel or name.startswith(kernel.split("<")[0] + "<")) and "hbm_bytes" in e:
+                return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
+    return None, None
 
 
 def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):
