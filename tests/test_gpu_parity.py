@@ -9,6 +9,8 @@ Parameter sets:
           fast basis conversion with alpha > 1, K > 1 and a partial digit;
           P = 2^118 exceeds every digit modulus, as hybrid switching needs)
   bench : config 2/3 sizes, n=2^16, L=8, K=1, dnum=8
+  bench_d2: the bench's own parameters, n=2^16, L=8, K=4, dnum=2
+  c5    : config 5 sizes, n=2^17, L=12, K=4, dnum=3 (the multi-GPU config)
 Integer results must match exactly; decoded values are compared with the
 closed-loop tolerance of the CSTR test (1e-6 relative, reference achieves
 1e-11).
@@ -26,6 +28,7 @@ PARAMS = {
     "bench": ("params", dict(logn=16, nlimbs=8, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
     "bench_d2": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=60, qi_bits=50,
                                 p_bits=60)),
+    "c5": ("params", dict(logn=17, nlimbs=12, nspecial=4, dnum=3, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
 }
 
 
@@ -121,13 +124,16 @@ def test_evaluation_ops(oracle, product, name):
         assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
 
 
-def test_ntt_batch_bitexact(oracle, product):
-    """Config 2 layout at n=2^16, L=8 on a 4-polynomial sample."""
+@pytest.mark.parametrize("name", ["bench", "c5"])
+def test_ntt_batch_bitexact(oracle, product, name):
+    """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain on a
+    4-polynomial sample: forward, then inverse (the roundtrip identity)."""
     import torch
-    init_both(oracle, product, "bench")
+    init_both(oracle, product, name)
     n, L, npolys = product.n, product.L, 4
     host = np.zeros(npolys * L * n, dtype=np.uint64)
     oracle.lib.poly_fill_uniform(host.ctypes.data, npolys, L, 99)
+    orig = host.copy()
     dev = torch.empty(npolys * L * n, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
     product.lib.poly_fill_uniform(dev.data_ptr(), npolys, L, 99)
@@ -141,12 +147,13 @@ def test_ntt_batch_bitexact(oracle, product):
     product.lib.poly_intt_batch(dev.data_ptr(), npolys, L)
     product.sync()
     assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "c5"])
 def test_mul_rescale_batch_bitexact(oracle, product, name):
-    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4) on 3
-    random-residue ciphertext pairs."""
+    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4) and
+    the config 5 op at n=2^17, L=12 on 3 random-residue ciphertext pairs."""
     import ctypes
     import torch
     init_both(oracle, product, name)
