@@ -782,19 +782,20 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
   const size_t d01_stride = 2 * lvl * n, d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n,
                acc_stride = 2 * nm * n;
   Ws d01(count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
-  k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
   if (k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED")) {
     Ws y(count * d2_stride);
     const int mode = rescale ? 1 : 0;
     const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
     const unsigned keep = rescale ? lvl - 1 : lvl;
-    k_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl,
-                      dn_fused ? keep : 0, dn_fused ? keep : nm);
+    k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride,
+                          (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, dn_fused ? keep : 0,
+                          dn_fused ? keep : nm);
     if (dn_fused) {
       k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, d01.p, lvl * n);
       return;
     }
   } else {
+    k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
     k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
     k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
     unsigned mods[GPQHE_MAXMOD];

@@ -264,11 +264,14 @@ void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t see
 void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 bool k_ks_fused_ok();
-// p_lo: P (d0, d1) is added to acc limbs t in [p_lo, lvl) only; the fused
-// ModDown adds the remaining d0/d1 terms after its division.  Limbs t >=
-// drop_lo leave after the inverse row pass (input of k_moddown_fused).
-void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
-                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo);
+// Tensor product of `count` pairs (a, b: pair i at + i*in_stride, c1 at +
+// in_pstride) + fused relinearization.  p_lo: P (d0, d1) is added to acc
+// limbs t in [p_lo, lvl) only; the fused ModDown adds the remaining d0/d1
+// terms after its division.  Limbs t >= drop_lo leave after the inverse row
+// pass (input of k_moddown_fused).
+void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
+                           const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
+                           const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo);
 // ModDown (mode 0 or 1) of X fused with the d0/d1 terms left out by
 // k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
 // must hold the inverse row pass of their NTT form; d01 poly p at d01 + p*d01_pstride

@@ -15,6 +15,8 @@
 // with one 8-byte word per lane, canonical residues in and out.
 #include "gpqhe_internal.h"
 
+#include <type_traits>
+
 #include <map>
 #include <string.h>
 #include <tuple>
@@ -1080,8 +1082,16 @@ struct UpTable {
   UpDigit *dig;   // [ndig]
   uint64_t *c;    // [ndig][8][nm]  [Qj/q_i]_t 2^64 mod q_t (Montgomery form)
   uint64_t *ysc;  // [lvl][2]       n^-1 [(Qj/q_i)^-1]_{q_i} + Shoup (folded into the INTT)
+  uint64_t *ysc1; // [lvl][2]       n1^-1 [(Qj/q_i)^-1]_{q_i}: INTT columns after tensor_rows
+  uint64_t *n2i;  // [lvl][2]       n2^-1 mod q_i (tensor_rows output scale)
   unsigned ndig, nm;
 };
+
+// Row length n2 of the fused kernels' 4-step split (n = n1 x n2).
+static unsigned ks_logn2()
+{
+  return G.logn >= 15 ? 8 : 7;
+}
 
 static std::map<unsigned, UpTable> g_up;
 
@@ -1125,11 +1135,27 @@ static UpTable &up_table(unsigned lvl)
     ysc[2 * i] = w;
     ysc[2 * i + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[i]);
   }
+  // row-form split: tensor_rows leaves n2^-1 rows^-1(d2); the column INTT then
+  // needs n1^-1 = n^-1 n2 in place of n^-1
+  std::vector<uint64_t> ysc1(2 * (size_t)lvl), n2i(2 * (size_t)lvl);
+  const uint64_t n2 = 1ull << ks_logn2();
+  for (unsigned i = 0; i < lvl; i++) {
+    const uint64_t w = hm_mul_mod(ysc[2 * i], n2 % G.q[i], G.q[i]);
+    ysc1[2 * i] = w;
+    ysc1[2 * i + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[i]);
+    const uint64_t v = hm_inv_mod(n2, G.q[i]);
+    n2i[2 * i] = v;
+    n2i[2 * i + 1] = (uint64_t)(((unsigned __int128)v << 64) / G.q[i]);
+  }
   UpTable tab;
   tab.ndig = ndig;
   tab.nm = nm;
   HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
   HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMalloc(&tab.ysc1, ysc1.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.ysc1, ysc1.data(), ysc1.size() * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMalloc(&tab.n2i, n2i.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.n2i, n2i.data(), n2i.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.dig, ndig * sizeof(UpDigit)));
   HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
   HIP_CHECK(hipMemcpy(tab.dig, dig.data(), ndig * sizeof(UpDigit), hipMemcpyHostToDevice));
@@ -1356,12 +1382,78 @@ __global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size
   }
 }
 
+// Tensor product fused with the inverse row pass of d2 (batched relinearize,
+// alpha <= 4): d0 = a0 b0 and d1 = a0 b1 + a1 b0 are stored as they are (NTT
+// domain); d2 = a1 b1 leaves as n2^-1 rows^-1(d2).  That is exactly the column
+// intermediate of the 4-step NTT: the forward row pass of it reproduces d2
+// (ks_rows uses it as the digit's own limb), and the inverse column pass with
+// n1^-1 completes the INTT (ks_cols4 loader).
+template <int LOGN2>
+__global__ void __launch_bounds__(256) tensor_rows_kernel(uint64_t *d01, size_t d01_stride, uint64_t *d2r,
+                                                           size_t d2_stride, const uint64_t *a, const uint64_t *b,
+                                                           size_t in_stride, size_t in_pstride, unsigned logn,
+                                                           unsigned lvl, unsigned count, const uint64_t *n2i, Tw2 tw,
+                                                           const ModConst *mcs)
+{
+  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / R;
+  // limb-major block order: one modulus' twiddles stay hot in L2
+  const unsigned blk = blockIdx.x, limb = blk / (count * tiles), rem = blk % (count * tiles);
+  const unsigned p = rem / tiles, tile = rem % tiles;
+  const ModConst mc = mcs[limb];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * R;
+  const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
+  const uint64_t *pa = a + p * in_stride + off, *pb = b + p * in_stride + off;
+  uint64_t *o0 = d01 + p * d01_stride + off, *o1 = o0 + ((size_t)lvl << logn);
+  const int th = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int e = th + 256 * i;
+    const uint64_t a0 = pa[e], a1 = pa[in_pstride + e], b0 = pb[e], b1 = pb[in_pstride + e];
+    o0[e] = mul_mod(a0, b0, mc);
+    o1[e] = add_mod(mul_mod(a0, b1, mc), mul_mod(a1, b0, mc), q);
+    lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = mul_mod(a1, b1, mc);
+  }
+  __syncthreads();
+  const uint64_t *itw2 = tw.inv + ((size_t)limb << (logn + 1));
+  {
+    const int g = th % (N2 / 16), rr = th / (N2 / 16);
+    uint64_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = lds[rr * SP + rswz(16 * g + k)];
+    inv_stages<4>(r, itw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      lds[rr * SP + rswz(16 * g + k)] = r[k];
+  }
+  __syncthreads();
+  const uint64_t w = n2i[2 * limb], wp = n2i[2 * limb + 1];
+  uint64_t *y = d2r + p * d2_stride + off;
+#pragma unroll
+  for (int it = 0; it < R / 16; it++) {
+    const int item = th + 256 * it, l = item % 16, rr = item / 16;
+    uint64_t r[EA];
+#pragma unroll
+    for (int k = 0; k < EA; k++)
+      r[k] = lds[rr * SP + rswz(l + 16 * k)];
+    inv_stages<LEA>(r, itw2, (uint64_t)(n1 + row0 + rr) << LOGN2, 4, q);
+#pragma unroll
+    for (int k = 0; k < EA; k++)
+      y[(rr << LOGN2) + l + 16 * k] = mul_shoup(r[k], w, wp, q);
+  }
+  (void)q2;
+}
+
 // Multi-target variant for digits of at most 4 limbs: the block loads its
 // (p, j, tile) digit values into registers once and converts them for NT
 // targets in turn (the single-target kernel re-reads them through L2 for every
 // target and waits on those loads most of its time).  Column tiles are double
 // buffered in LDS, so one barrier per target suffices.
-template <int LOGT, int NT>
+template <int LOGT, int NT, bool INVC>
 __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
                                                            size_t t1_stride, unsigned logn, unsigned lvl,
                                                            unsigned L, unsigned nm, unsigned ndig, unsigned members,
@@ -1383,14 +1475,66 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
   const uint64_t *yb = ybuf + p * y_stride + ((size_t)lo << logn) + (size_t)tile * C;
   const int th = threadIdx.x;
   uint64_t y[IT][4][EA];
+  if constexpr (!INVC) {
 #pragma unroll
-  for (int it = 0; it < IT; it++) {
-    const int item = th + 256 * it, c = item % C, l = item / C;
+    for (int it = 0; it < IT; it++) {
+      const int item = th + 256 * it, c = item % C, l = item / C;
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+      for (int i = 0; i < 4; i++)
 #pragma unroll
-      for (int k = 0; k < EA; k++)
-        y[it][i][k] = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+        for (int k = 0; k < EA; k++)
+          y[it][i][k] = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+    }
+  } else {
+    // the digit arrives after the inverse row pass (tensor_rows_kernel): run
+    // the inverse column pass with n1^-1 [(Qj/q_i)^-1] here, limb by limb
+    auto load_limb = [&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if (i >= (int)na) {
+#pragma unroll
+        for (int it = 0; it < IT; it++)
+#pragma unroll
+          for (int k = 0; k < EA; k++)
+            y[it][i][k] = 0;
+        return;
+      }
+      const unsigned mi_ = lo + i;
+      const uint64_t qi = mcs[mi_].q;
+      const uint64_t *itw2 = tw.inv + ((size_t)mi_ << (logn + 1));
+      const uint64_t w = tab.ysc1[2 * mi_], wp = tab.ysc1[2 * mi_ + 1];
+      const uint64_t *src = yb + ((size_t)i << logn);
+      if (i)
+        __syncthreads();
+      {
+        const int c = th % C, g = th / C;
+        uint64_t r[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          r[k] = src[(size_t)(16 * g + k) * n2 + c];
+        inv_stages<4>(r, itw2, T + 16 * g, 0, qi);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          lds[0][(16 * g + k) * CP + c] = r[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        const int item = th + 256 * it, c = item % C, l = item / C;
+        uint64_t r[EA];
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          r[k] = lds[0][(l + 16 * k) * CP + c];
+        inv_stages<LEA>(r, itw2, T, 4, qi);
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          y[it][i][k] = mul_shoup(r[k], w, wp, qi);
+      }
+    };
+    load_limb(std::integral_constant<int, 0>{});
+    load_limb(std::integral_constant<int, 1>{});
+    load_limb(std::integral_constant<int, 2>{});
+    load_limb(std::integral_constant<int, 3>{});
+    __syncthreads();
   }
   for (int u = 0; u < NT; u++) {
     const unsigned ui = mi * NT + u;
@@ -1455,7 +1599,8 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                        unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
-                                                       unsigned p_lo, unsigned drop_lo, Tw2 tw, const ModConst *mcs)
+                                                       unsigned p_lo, unsigned drop_lo, int own_rowform, Tw2 tw,
+                                                       const ModConst *mcs)
 {
   constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
@@ -1514,10 +1659,13 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
     const uint64_t *eb = evkm + (((size_t)(2 * j) * nmod + m) << logn) + toff + th;
     const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
     uint64_t r[16];
-    if (t < lvl && t / alpha == j) {
+    const bool own = t < lvl && t / alpha == j;
+    if (own && !own_rowform) {
       load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, r);  // own digit: NTT-form d2
     } else {
-      const uint64_t *x = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+      // converted limb from ks_cols, or (row form) the own d2 limb's column intermediate
+      const uint64_t *x = own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
+                              : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
       __syncthreads();
 #pragma unroll
       for (int it = 0; it < R / 16; it++) {
@@ -1605,7 +1753,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
                             const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
-                            unsigned drop_lo)
+                            unsigned drop_lo, bool rowform)
 {
   UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
@@ -1615,28 +1763,47 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   const unsigned tiles = n / 4096;
   const double own = (double)G.alpha * ndig;  // digit slots not converted (approx. for partial digits)
   {
-    // reads the digit's alpha limbs once per target tile set (L2), writes the
-    // converted + column-transformed limb
+    // reads the digit's alpha limbs once per target set (registers), writes
+    // the converted + column-transformed limbs
     ProfScope ps(KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
     const unsigned ngroups = tiles * count * ndig;
-    if (G.alpha <= 4 && !getenv("GPQHE_KSCOLS1")) {
-      constexpr unsigned NT = 4;
-      const unsigned na_min = lvl - (ndig - 1) * G.alpha;  // the last digit may be partial
+    if (rowform) {
+      constexpr unsigned NT = 8;  // all targets of a digit tile: its INTT columns run once
+      const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
-      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream,
-                         y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw,
-                         G.dev.mc);
+      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
+                         G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
+                         tw, G.dev.mc);
+    } else if (G.alpha <= 4) {
+      constexpr unsigned NT = 4;
+      const unsigned na_min = lvl - (ndig - 1) * G.alpha;
+      const unsigned members = (nm - na_min + NT - 1) / NT;
+      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
+                         G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
+                         tw, G.dev.mc);
     } else {
       hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
     }
   }
-  // reads T1 (+ own d2 limbs, d0/d1) per ciphertext and the key once, writes acc
+  // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key once, writes acc
   ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
                                                        2 * nm) + 2.0 * ndig * nm));
   hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * tiles)), dim3(256), 0, G.stream, T1,
                      t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
-                     ndig, G.alpha, count, p_lo, drop_lo, tw, G.dev.mc);
+                     ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int LOGN2>
+static void tensor_rows_launch(uint64_t *d01, uint64_t *d2r, const uint64_t *a, const uint64_t *b, size_t in_stride,
+                               size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab)
+{
+  ProfScope ps(KC_TENSOR, 8.0 * G.n * lvl * count * 7);  // read 4 limbs, write 3 limbs
+  const Tw2 tw{G.tw2, G.itw2};
+  hipLaunchKernelGGL((tensor_rows_kernel<LOGN2>), dim3(lvl * count * (G.n / 4096)), dim3(256), 0, G.stream, d01,
+                     (size_t)2 * lvl * G.n, d2r, (size_t)lvl * G.n, a, b, in_stride, in_pstride, G.logn, lvl, count,
+                     tab.n2i, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1645,29 +1812,42 @@ bool k_ks_fused_ok()
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
 }
 
-// Fused relinearization core for `count` ciphertexts: d01 [count][2][lvl],
-// d2n [count][lvl] (NTT form), ybuf/T1 workspaces; writes acc [count][2][nm].
-void k_keyswitch_fused(uint64_t *acc, const uint64_t *d01, const uint64_t *d2n, uint64_t *ybuf, uint64_t *T1,
-                       const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo)
+// Tensor product + fused relinearization core for `count` ciphertext pairs:
+// writes d01 [count][2][lvl] and acc [count][2][nm]; d2 [count][lvl], ybuf and
+// T1 are workspaces.
+void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
+                           const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
+                           const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo)
 {
   UpTable &tab = up_table(lvl);
-  unsigned mods[GPQHE_MAXMOD];
-  for (unsigned i = 0; i < lvl; i++)
-    mods[i] = i;
-  LimbSet in{}, out{};
-  in.base = (uint64_t *)d2n;
-  out.base = ybuf;
-  in.stride = out.stride = (size_t)lvl * G.n;
-  in.per = out.per = lvl;
-  in.count = out.count = lvl * count;
-  for (unsigned i = 0; i < lvl; i++)
-    in.mods[i] = out.mods[i] = (uint8_t)mods[i];
-  k_ntt_ex(in, out, true, tab.ysc);
+  // Row form removes the d2 INTT but lengthens the (latency-bound) tensor,
+  // ks_cols and ks_rows kernels by more than it saves (20.1k vs 20.7k op/s at
+  // N=2^16, L=8); opt-in until those kernels are pipelined.
+  const bool rowform = G.alpha <= 4 && getenv("GPQHE_KS_ROWFORM");
+  if (rowform) {
+    // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
+    if (ks_logn2() == 8)
+      tensor_rows_launch<8>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
+    else
+      tensor_rows_launch<7>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
+  } else {
+    k_tensor(d01, d2, a, b, lvl, in_stride, in_pstride, count, (size_t)2 * lvl * G.n);
+    LimbSet in{}, out{};
+    in.base = d2;
+    out.base = ybuf;
+    in.stride = out.stride = (size_t)lvl * G.n;
+    in.per = out.per = lvl;
+    in.count = out.count = lvl * count;
+    for (unsigned i = 0; i < lvl; i++)
+      in.mods[i] = out.mods[i] = (uint8_t)i;
+    k_ntt_ex(in, out, true, tab.ysc);
+  }
+  const uint64_t *y = rowform ? d2 : ybuf;
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
-  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
-  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
-  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2n, d01, evkm, acc, count, lvl, p_lo, drop_lo); break;
+  case 13: ks_fused_launch<6, 7>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 14: ks_fused_launch<7, 7>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 15: ks_fused_launch<7, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 16: ks_fused_launch<8, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^16");
   }
 }
@@ -1692,7 +1872,7 @@ __global__ void to_mont_kernel(uint64_t *out, const uint64_t *in, unsigned logn,
 // nmod), laid out for ks_rows when the fused path serves this ring degree.
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
 {
-  const unsigned logn2 = k_ks_fused_ok() ? (G.logn >= 15 ? 8 : 7) : 0;
+  const unsigned logn2 = k_ks_fused_ok() ? ks_logn2() : 0;
   hipLaunchKernelGGL(to_mont_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs_total), dim3(TPB), 0, G.stream, out, in,
                      G.logn, G.nmod, logn2, G.dev.mc);
   HIP_CHECK(hipGetLastError());
@@ -2198,6 +2378,8 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.dig));
     HIP_CHECK(hipFree(kv.second.c));
     HIP_CHECK(hipFree(kv.second.ysc));
+    HIP_CHECK(hipFree(kv.second.ysc1));
+    HIP_CHECK(hipFree(kv.second.n2i));
   }
   g_up.clear();
   for (auto &kv : g_down) {

@@ -150,12 +150,16 @@ def test_ntt_batch_bitexact(oracle, product, name):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "c5"])
-def test_mul_rescale_batch_bitexact(oracle, product, name):
-    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4) and
-    the config 5 op at n=2^17, L=12 on 3 random-residue ciphertext pairs."""
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "c5"])
+def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
+    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
+    latter also through the opt-in row-form key switch) and the config 5 op at
+    n=2^17, L=12 on 3 random-residue ciphertext pairs."""
     import ctypes
     import torch
+    if name.endswith("_rowform"):
+        monkeypatch.setenv("GPQHE_KS_ROWFORM", "1")
+        name = name[:-len("_rowform")]
     init_both(oracle, product, name)
     n, L, cnt = product.n, product.L, 3
     _, _, _, rlk_o = keys(oracle, rot=False)
