@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cstr", action="store_true", help="skip the encrypted CSTR loop (config 4)")
     ap.add_argument("--cstr-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-ntt", action="store_true", help="skip the NTT roundtrip leg (config 2)")
+    ap.add_argument("--ntt-polys", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration")
     return ap.parse_args()
 
@@ -165,6 +167,8 @@ def main():
             "kernels": kernels,
             "instrumented_ms_per_step": 1e3 * (ti1 - ti0) / args.steps,
         }
+    if rank == 0 and not args.no_ntt:
+        result["ntt_roundtrip"] = ntt_roundtrip(eng, stream, logn, L, args.ntt_polys)
     barrier()
     if rank == 0 and not args.no_cstr:
         eng.exit()
@@ -197,6 +201,32 @@ def pmc_traffic(kernel, workload):
             if (name == kernel or name.startswith(kernel.split("<")[0] + "<")) and "hbm_bytes" in e:
                 return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
     return None, None
+
+
+def ntt_roundtrip(eng, stream, logn, L, polys, reps=3):
+    """Config 2: forward + inverse NTT of `polys` polynomials x L limbs at
+    N=2^logn resident in HBM (poly_ntt_batch / poly_intt_batch), timed with
+    HIP events on the engine stream; algorithmic bytes = read + write of every
+    limb per transform (twiddles amortised), i.e. 16 n L bytes per poly."""
+    import torch
+    n = 1 << logn
+    buf = torch.empty(polys * L * n, dtype=torch.int64, device="cuda")
+    eng.lib.poly_fill_uniform(buf.data_ptr(), polys, L, 0x48454354520001)
+    eng.lib.poly_ntt_batch(buf.data_ptr(), polys, L)
+    eng.lib.poly_intt_batch(buf.data_ptr(), polys, L)
+    eng.sync()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(reps):
+        eng.lib.poly_ntt_batch(buf.data_ptr(), polys, L)
+        eng.lib.poly_intt_batch(buf.data_ptr(), polys, L)
+    ev1.record(stream)
+    eng.sync()
+    dt = ev0.elapsed_time(ev1) / 1e3 / reps
+    alg = 2.0 * 2 * 8 * n * L * polys  # two transforms, each reads + writes every limb once
+    del buf
+    return {"polys": polys, "nlimbs": L, "logn": logn, "roundtrip_ms": 1e3 * dt, "polys_per_s": polys / dt,
+            "alg_GBs": alg / dt / 1e9, "frac_of_8TBs": alg / dt / 8e12}
 
 
 def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):

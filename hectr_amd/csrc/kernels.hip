@@ -640,6 +640,177 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, LimbSet o, un
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row pass, 8 elements per thread: tile = R x N2 with R N2 = 2048 (16 KiB of
+// LDS, no padding), three register rounds of 3, 3 and LOGN2 - 6 stages.
+// Half the registers of the 16-element form, so twice the waves per CU to
+// overlap one block's butterflies with another's loads.
+//   round A: thread (row, l < TA = N2/8)    elements l + TA k
+//   round B: thread (row, m < 8, l' < TA/8) elements m TA + l' + (TA/8) k
+//   round C: thread (row, h < TA)           elements 8 h + k (consecutive)
+// LDS swizzle (conflict-free for all four access patterns, checked offline):
+// column c of row r sits at c ^ ((c >> 3) & (TA - 1)) (^ (r & 1) << 4 for
+// N2 = 128).
+// ---------------------------------------------------------------------------
+template <int LOGN2>
+struct Row8 {
+  static constexpr int N2 = 1 << LOGN2, R = 2048 / N2, TA = N2 / 8, TB = TA / 8, EC = 1 << (LOGN2 - 6);
+  static __device__ __forceinline__ int at(int row, int c)
+  {
+    int x = c ^ ((c >> 3) & (TA - 1));
+    if (LOGN2 == 7)
+      x ^= (row & 1) << 4;
+    return row * N2 + x;
+  }
+};
+
+// forward row pass of one tile, rounds A..C; round A input in r (thread's A
+// elements), result in r (thread's C elements, canonical)
+template <int LOGN2>
+__device__ __forceinline__ void rows8_fwd(uint64_t (&r)[8], uint64_t *lds, const uint64_t *tw2, uint64_t rowbase0,
+                                          uint64_t q)
+{
+  using T = Row8<LOGN2>;
+  const int th = threadIdx.x, row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int l = th % T::TA;
+    fwd_stages<3>(r, tw2, rb, LOGN2 - 1, q);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, l + T::TA * k)] = r[k];
+  }
+  __syncthreads();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, c0 + T::TB * k)];
+    fwd_stages<3>(r, tw2, rb + mb * T::TA, LOGN2 - 4, q);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, c0 + T::TB * k)] = r[k];
+  }
+  __syncthreads();
+  {
+    const int h = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, 8 * h + k)];
+#pragma unroll
+    for (int j = 0; j < 8 / T::EC; j++) {
+      uint64_t g[T::EC];
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        g[e] = r[j * T::EC + e];
+      fwd_stages<LOGN2 - 6>(g, tw2, rb + 8 * h + T::EC * j, LOGN2 - 7, q);
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        r[j * T::EC + e] = canon4(g[e], q, 2 * q);
+    }
+  }
+}
+
+// inverse row pass of one tile: input r = thread's C elements (< 2q), result
+// r = thread's A elements (< 2q, not canonical)
+template <int LOGN2>
+__device__ __forceinline__ void rows8_inv(uint64_t (&r)[8], uint64_t *lds, const uint64_t *itw2, uint64_t rowbase0,
+                                          uint64_t q)
+{
+  using T = Row8<LOGN2>;
+  const int th = threadIdx.x, row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int h = th % T::TA;
+#pragma unroll
+    for (int j = 0; j < 8 / T::EC; j++) {
+      uint64_t g[T::EC];
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        g[e] = r[j * T::EC + e];
+      inv_stages<LOGN2 - 6>(g, itw2, rb + 8 * h + T::EC * j, 0, q);
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        r[j * T::EC + e] = g[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, 8 * h + k)] = r[k];
+  }
+  __syncthreads();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, c0 + T::TB * k)];
+    inv_stages<3>(r, itw2, rb + mb * T::TA, LOGN2 - 6, q);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, c0 + T::TB * k)] = r[k];
+  }
+  __syncthreads();
+  {
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, l + T::TA * k)];
+    inv_stages<3>(r, itw2, rb, LOGN2 - 3, q);
+  }
+}
+
+template <int LOGN2, bool INV>
+__global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+                                                         const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  unsigned v, tile;
+  pm_decode(s, n1 / T::R, v, tile);
+  const unsigned m = s.mod(v);
+  const uint64_t q = mcs[m].q, q2 = 2 * q;
+  const unsigned row0 = tile * T::R;
+  const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
+  uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
+  const int th = threadIdx.x, row = th / T::TA;
+  uint64_t r[8];
+  if constexpr (!INV) {
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = x[(row << LOGN2) + l + T::TA * k];
+    rows8_fwd<LOGN2>(r, lds, tw.fwd + ((size_t)m << (logn + 1)), n1 + row0, q);
+    const int h = th % T::TA;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, 8 * h + k)] = r[k];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int e = th + 256 * i;
+      y[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int e = th + 256 * i;
+      lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = x[e];
+    }
+    __syncthreads();
+    const int h = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, 8 * h + k)];
+    __syncthreads();
+    rows8_inv<LOGN2>(r, lds, tw.inv + ((size_t)m << (logn + 1)), n1 + row0, q);
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      y[(row << LOGN2) + l + T::TA * k] = canon4(r[k], q, q2);
+  }
+}
+
 template <int LOGT1, int LOGN2>
 static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const uint64_t *post)
 {
@@ -647,6 +818,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const unsigned blocks = s.count * (n / 4096);
   const Tw2 tw{G.tw2, G.itw2};
   const double pass_bytes = 16.0 * n * s.count;
+  static const bool rows8 = !getenv("GPQHE_NTT2ROWS");
   if (!inverse) {
     {
       ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
@@ -654,13 +826,21 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
                          G.dev.mc, (const uint64_t *)nullptr);
     }
     ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
-    hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
-                       G.dev.mc);
+    if (rows8)
+      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
+                         G.dev.mc);
+    else
+      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
+                         G.dev.mc);
   } else {
     {
       ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
-      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
-                         G.dev.mc);
+      if (rows8)
+        hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn,
+                           tw, G.dev.mc);
+      else
+        hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
+                           G.dev.mc);
     }
     ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
     hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,

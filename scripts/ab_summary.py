@@ -12,5 +12,8 @@ for f in sorted(glob.glob(f"gpurun_out/{sys.argv[1]}/bench_*.log")):
     ks = sorted(d.get("kernels", {}).items(), key=lambda kv: -kv[1]["share"])
     print(f"{f.split('/')[-1]:24s} {d['value']:9.0f} {d['unit']}  dom={d['roofline']['kernel']} "
           f"{d['roofline']['achieved']:.0f} GB/s")
+    if "ntt_roundtrip" in d:
+        t = d["ntt_roundtrip"]
+        print(f"    ntt roundtrip {t['polys']} polys: {t['roundtrip_ms']:.2f} ms, {t['alg_GBs']:.0f} GB/s")
     for k, v in ks:
         print(f"    {k:28s} {v['avg_us']:8.1f} us  {v['share']*100:5.1f}%  {v['GBs']:7.0f} GB/s")

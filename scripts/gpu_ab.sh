@@ -11,8 +11,8 @@ rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log; [ $rc -eq 0 ] || exit 1
 for v in base ${VARIANTS}; do
   name=${v%%=*}; kv=${v#*=}
   if [ "$v" = base ]; then
-    timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-cstr ${BENCH_ARGS} > $OUT/bench_base.log 2>&1 || exit 1
+    timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-cstr --ntt-polys 256 ${BENCH_ARGS} > $OUT/bench_base.log 2>&1 || exit 1
   else
-    env "$kv" timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-cstr ${BENCH_ARGS} > $OUT/bench_$name.log 2>&1 || exit 1
+    env "$kv" timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-cstr --ntt-polys 256 ${BENCH_ARGS} > $OUT/bench_$name.log 2>&1 || exit 1
   fi
 done
