@@ -202,6 +202,7 @@ struct Context {
   uint64_t counter = 0;
   DevTables dev{};
   const uint64_t *tw2 = nullptr, *itw2 = nullptr;  // interleaved (w, w') pairs [nmod][n][2]
+  const double *twd = nullptr, *itwd = nullptr;    // interleaved (w, w / q) doubles [nmod][n][2]
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;
   int device = 0;

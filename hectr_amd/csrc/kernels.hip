@@ -394,8 +394,10 @@ __global__ void __launch_bounds__(TPB) ntt_rows_kernel(LimbSet s, unsigned logn,
 // the workgroups resident at one time share one prime's twiddle table.
 // ===========================================================================
 struct Tw2 {
-  const uint64_t *fwd;  // [nmod][n][2]
+  const uint64_t *fwd;  // [nmod][n][2] (w, floor(w 2^64 / q))
   const uint64_t *inv;
+  const double *fwdd;   // [nmod][n][2] (w, w / q) as doubles (moduli < 2^50)
+  const double *invd;
 };
 
 __device__ __forceinline__ uint64_t lazy_lt2q(uint64_t x, uint64_t q2)
@@ -459,6 +461,125 @@ __device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_
   }
 }
 
+// ---------------------------------------------------------------------------
+// FP64 butterflies for moduli q < 2^50 (the FP64 pipe is full rate on gfx950
+// and twice as fast as 64-bit integer Shoup per butterfly, scripts/ubench_bfly).
+// Values are signed doubles holding exact integers:
+//   mulmod: h = fl(y w), l = fma(y, w, -h) (exact), qt = rint(y fl(w/q)),
+//           T = fma(-qt, q, h) + l = y w - qt q exactly.  With |y| <= 1.5 q,
+//           |y w / q - qt| <= 1/2 + 1.5 q 2^-52 < 0.875, so |T| < 0.875 q.
+//   red:    x - rint(x fl(1/q)) q, |result| <= q/2 (+ negligible).
+// CT: X = red(x[k]), T = mulmod(x[k+h]); outputs X +- T, |.| < 1.375 q.
+// GS: outputs red(U + V) and mulmod(U - V) with |U|, |V| <= q.
+// Every intermediate is an integer below 2^53, so the residues are exact and
+// the canonical outputs equal the integer path's bit for bit.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double f64_mulmod(double y, double w, double wq, double q)
+{
+  const double h = y * w;
+  const double l = __fma_rn(y, w, -h);
+  const double qt = rint(y * wq);
+  return __fma_rn(-qt, q, h) + l;
+}
+
+__device__ __forceinline__ double f64_red(double x, double q, double qinv)
+{
+  return __fma_rn(-rint(x * qinv), q, x);
+}
+
+template <int LE>
+__device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
+                                             int log_thi, double q, double qinv)
+{
+  constexpr int E = 1 << LE;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_thi - s + 1);
+    const int half = E >> (s + 1);
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
+      const double X = f64_red(x[k], q, qinv);
+      const double T = f64_mulmod(x[k + half], twd[i2], twd[i2 + 1], q);
+      x[k] = X + T;
+      x[k + half] = X - T;
+    }
+  }
+}
+
+template <int LE>
+__device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
+                                             int log_tlo, double q, double qinv)
+{
+  constexpr int E = 1 << LE;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_tlo + s + 1);
+    const int half = 1 << s;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
+      const double U = x[k], V = x[k + half];
+      x[k] = f64_red(U + V, q, qinv);
+      x[k + half] = f64_mulmod(U - V, twd[i2], twd[i2 + 1], q);
+    }
+  }
+}
+
+// Arithmetic policies: the NTT kernels are written once against these.  Both
+// read and write canonical u64 residues; ArF64 requires q < 2^50.
+struct ArInt {
+  using V = uint64_t;
+  uint64_t q;
+  const uint64_t *tw;  // this modulus' (w, w') pairs
+  __device__ static V load(uint64_t x) { return x; }
+  __device__ uint64_t canon(V x) const { return canon4(x, q, 2 * q); }  // x < 4q
+  __device__ static uint64_t bits(V x) { return x; }
+  __device__ static V unbits(uint64_t b) { return b; }
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const { fwd_stages<LE>(x, tw, bb, log_thi, q); }
+  template <int LE>
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, tw, bb, log_tlo, q); }
+  // canonical x w for a constant w < q (Shoup pair)
+  __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
+};
+
+struct ArF64 {
+  using V = double;
+  double q, qinv;
+  const double *tw;  // this modulus' (w, w / q) pairs
+  __device__ static V load(uint64_t x) { return (double)x; }
+  __device__ uint64_t canon(V x) const
+  {
+    double v = f64_red(x, q, qinv);
+    v = v < 0 ? v + q : v;
+    return (uint64_t)v;
+  }
+  __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
+  __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv);
+  }
+  template <int LE>
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  {
+    inv_stages_f<LE>(x, tw, bb, log_tlo, q, qinv);
+  }
+  __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
+  {
+    const double wd = (double)w;
+    return canon(f64_mulmod(x, wd, wd / q, q));
+  }
+};
+
+constexpr uint64_t F64_QMAX = 1ull << 50;  // ArF64 applies to moduli below this
+
 // Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
 // B reads 16 consecutive columns per thread at a 16-column lane stride; the
 // XOR spreads those lanes over distinct banks (8-way conflict without it).
@@ -481,78 +602,93 @@ __device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsi
 }
 
 // Column pass: tile = T rows x C columns (T C = 4096).
+template <int LOGT, bool INV, class A>
+__device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64_t *y, unsigned n2, uint64_t *lds,
+                                          uint64_t sw, uint64_t swp)
+{
+  using V = typename A::V;
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
+  const int t = threadIdx.x;
+  if constexpr (!INV) {
+    // round A: rows l + 16 k (distances T/2 .. 16)
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      V r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = A::load(x[(size_t)(l + 16 * k) * n2 + c]);
+      ar.template fwd<LEA>(r, T, LOGT - 1);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        lds[(l + 16 * k) * CP + c] = A::bits(r[k]);
+    }
+    __syncthreads();
+    // round B: rows 16 g + k (distances 8 .. 1)
+    const int c = t % C, g = t / C;
+    V r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = A::unbits(lds[(16 * g + k) * CP + c]);
+    ar.template fwd<4>(r, T + 16 * g, 3);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      y[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+  } else {
+    {
+      const int c = t % C, g = t / C;
+      V r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = A::load(x[(size_t)(16 * g + k) * n2 + c]);
+      ar.template inv<4>(r, T + 16 * g, 0);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[(16 * g + k) * CP + c] = A::bits(r[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      V r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = A::unbits(lds[(l + 16 * k) * CP + c]);
+      ar.template inv<LEA>(r, T, 4);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        y[(size_t)(l + 16 * k) * n2 + c] = ar.mulc(r[k], sw, swp);
+    }
+  }
+}
+
 template <int LOGT, bool INV>
 __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                          const ModConst *mcs, const uint64_t *post)
 {
-  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
+  constexpr int T = 1 << LOGT, C = 4096 / T, CP = C + 1;
   __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
   const unsigned n2 = 1u << (logn - LOGT);
   unsigned v, tile;
   pm_decode(s, n2 / C, v, tile);
   const unsigned m = s.mod(v);
   const ModConst mc = mcs[m];
-  const uint64_t q = mc.q, q2 = 2 * q;
   const uint64_t *x = s.limb(v, logn) + (size_t)tile * C;
   uint64_t *y = o.limb(v, logn) + (size_t)tile * C;
-  const int t = threadIdx.x;
-  if constexpr (!INV) {
-    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
-    // round A: rows l + 16 k (distances T/2 .. 16)
-#pragma unroll
-    for (int it = 0; it < C / 16; it++) {
-      const int item = t + 256 * it, c = item % C, l = item / C;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = x[(size_t)(l + 16 * k) * n2 + c];
-      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        lds[(l + 16 * k) * CP + c] = r[k];
-    }
-    __syncthreads();
-    // round B: rows 16 g + k (distances 8 .. 1)
-    {
-      const int c = t % C, g = t / C;
-      uint64_t r[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = lds[(16 * g + k) * CP + c];
-      fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        y[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
-    }
+  // final scale of the inverse: n^-1, or a caller constant per limb slot (e.g.
+  // n^-1 times the ModUp factor [(Q_j/q_i)^-1]_{q_i}, folded into the INTT)
+  uint64_t sw = 0, swp = 0;
+  if (INV) {
+    sw = post ? post[2 * (v % s.per)] : mc.ninv;
+    swp = post ? post[2 * (v % s.per) + 1] : mc.ninvp;
+  }
+  const size_t toff = (size_t)m << (logn + 1);
+  if (mc.q < F64_QMAX) {
+    const ArF64 ar{(double)mc.q, 1.0 / (double)mc.q, (INV ? tw.invd : tw.fwdd) + toff};
+    cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp);
   } else {
-    const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
-    {
-      const int c = t % C, g = t / C;
-      uint64_t r[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = x[(size_t)(16 * g + k) * n2 + c];
-      inv_stages<4>(r, tw2, T + 16 * g, 0, q);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        lds[(16 * g + k) * CP + c] = r[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < C / 16; it++) {
-      const int item = t + 256 * it, c = item % C, l = item / C;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = lds[(l + 16 * k) * CP + c];
-      inv_stages<LEA>(r, tw2, T, 4, q);
-      // final scale: n^-1, or a caller constant per limb slot (e.g. n^-1 times
-      // the ModUp factor [(Q_j/q_i)^-1]_{q_i}, folded into the INTT)
-      const uint64_t sw = post ? post[2 * (v % s.per)] : mc.ninv, swp = post ? post[2 * (v % s.per) + 1] : mc.ninvp;
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        y[(size_t)(l + 16 * k) * n2 + c] = mul_shoup(r[k], sw, swp, q);
-    }
+    const ArInt ar{mc.q, (INV ? tw.inv : tw.fwd) + toff};
+    cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp);
   }
 }
 
@@ -664,127 +800,120 @@ struct Row8 {
   }
 };
 
-// forward row pass of one tile, rounds A..C; round A input in r (thread's A
-// elements), result in r (thread's C elements, canonical)
-template <int LOGN2>
-__device__ __forceinline__ void rows8_fwd(uint64_t (&r)[8], uint64_t *lds, const uint64_t *tw2, uint64_t rowbase0,
-                                          uint64_t q)
+// forward row pass of one tile, rounds A..C: round A input in r (the
+// thread's A elements), canonical result in out (the thread's C elements)
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)[8], uint64_t *lds, const A &ar,
+                                          uint64_t rowbase0)
 {
   using T = Row8<LOGN2>;
+  using V = typename A::V;
   const int th = threadIdx.x, row = th / T::TA;
   const uint64_t rb = (rowbase0 + row) << LOGN2;
   {
     const int l = th % T::TA;
-    fwd_stages<3>(r, tw2, rb, LOGN2 - 1, q);
+    ar.template fwd<3>(r, rb, LOGN2 - 1);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      lds[T::at(row, l + T::TA * k)] = r[k];
+      lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
   }
   __syncthreads();
   {
     const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = lds[T::at(row, c0 + T::TB * k)];
-    fwd_stages<3>(r, tw2, rb + mb * T::TA, LOGN2 - 4, q);
+      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
+    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      lds[T::at(row, c0 + T::TB * k)] = r[k];
+      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
   }
   __syncthreads();
-  {
-    const int h = th % T::TA;
+  const int h = th % T::TA;
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = lds[T::at(row, 8 * h + k)];
+  for (int k = 0; k < 8; k++)
+    r[k] = A::unbits(lds[T::at(row, 8 * h + k)]);
 #pragma unroll
-    for (int j = 0; j < 8 / T::EC; j++) {
-      uint64_t g[T::EC];
+  for (int j = 0; j < 8 / T::EC; j++) {
+    V g[T::EC];
 #pragma unroll
-      for (int e = 0; e < T::EC; e++)
-        g[e] = r[j * T::EC + e];
-      fwd_stages<LOGN2 - 6>(g, tw2, rb + 8 * h + T::EC * j, LOGN2 - 7, q);
+    for (int e = 0; e < T::EC; e++)
+      g[e] = r[j * T::EC + e];
+    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
 #pragma unroll
-      for (int e = 0; e < T::EC; e++)
-        r[j * T::EC + e] = canon4(g[e], q, 2 * q);
-    }
+    for (int e = 0; e < T::EC; e++)
+      out[j * T::EC + e] = ar.canon(g[e]);
   }
 }
 
-// inverse row pass of one tile: input r = thread's C elements (< 2q), result
-// r = thread's A elements (< 2q, not canonical)
-template <int LOGN2>
-__device__ __forceinline__ void rows8_inv(uint64_t (&r)[8], uint64_t *lds, const uint64_t *itw2, uint64_t rowbase0,
-                                          uint64_t q)
+// inverse row pass of one tile: input r = thread's C elements (canonical or
+// bounded as the policy's inverse allows), result r = thread's A elements
+// (lazy; canonicalise with ar.canon)
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0)
 {
   using T = Row8<LOGN2>;
+  using V = typename A::V;
   const int th = threadIdx.x, row = th / T::TA;
   const uint64_t rb = (rowbase0 + row) << LOGN2;
   {
     const int h = th % T::TA;
 #pragma unroll
     for (int j = 0; j < 8 / T::EC; j++) {
-      uint64_t g[T::EC];
+      V g[T::EC];
 #pragma unroll
       for (int e = 0; e < T::EC; e++)
         g[e] = r[j * T::EC + e];
-      inv_stages<LOGN2 - 6>(g, itw2, rb + 8 * h + T::EC * j, 0, q);
+      ar.template inv<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, 0);
 #pragma unroll
       for (int e = 0; e < T::EC; e++)
         r[j * T::EC + e] = g[e];
     }
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      lds[T::at(row, 8 * h + k)] = r[k];
+      lds[T::at(row, 8 * h + k)] = A::bits(r[k]);
   }
   __syncthreads();
   {
     const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = lds[T::at(row, c0 + T::TB * k)];
-    inv_stages<3>(r, itw2, rb + mb * T::TA, LOGN2 - 6, q);
+      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
+    ar.template inv<3>(r, rb + mb * T::TA, LOGN2 - 6);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      lds[T::at(row, c0 + T::TB * k)] = r[k];
+      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
   }
   __syncthreads();
   {
     const int l = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = lds[T::at(row, l + T::TA * k)];
-    inv_stages<3>(r, itw2, rb, LOGN2 - 3, q);
+      r[k] = A::unbits(lds[T::at(row, l + T::TA * k)]);
+    ar.template inv<3>(r, rb, LOGN2 - 3);
   }
 }
 
-template <int LOGN2, bool INV>
-__global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
-                                                         const ModConst *mcs)
+template <int LOGN2, bool INV, class A>
+__device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint64_t *y, uint64_t *lds,
+                                           uint64_t rowbase0)
 {
   using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
-  const unsigned n1 = 1u << (logn - LOGN2);
-  unsigned v, tile;
-  pm_decode(s, n1 / T::R, v, tile);
-  const unsigned m = s.mod(v);
-  const uint64_t q = mcs[m].q, q2 = 2 * q;
-  const unsigned row0 = tile * T::R;
-  const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
-  uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
+  using V = typename A::V;
   const int th = threadIdx.x, row = th / T::TA;
-  uint64_t r[8];
+  V r[8];
   if constexpr (!INV) {
     const int l = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = x[(row << LOGN2) + l + T::TA * k];
-    rows8_fwd<LOGN2>(r, lds, tw.fwd + ((size_t)m << (logn + 1)), n1 + row0, q);
+      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+    uint64_t out[8];
+    rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0);
     const int h = th % T::TA;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      lds[T::at(row, 8 * h + k)] = r[k];
+      lds[T::at(row, 8 * h + k)] = out[k];
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -801,13 +930,37 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
     const int h = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = lds[T::at(row, 8 * h + k)];
+      r[k] = A::load(lds[T::at(row, 8 * h + k)]);
     __syncthreads();
-    rows8_inv<LOGN2>(r, lds, tw.inv + ((size_t)m << (logn + 1)), n1 + row0, q);
+    rows8_inv<LOGN2>(r, lds, ar, rowbase0);
     const int l = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      y[(row << LOGN2) + l + T::TA * k] = canon4(r[k], q, q2);
+      y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+  }
+}
+
+template <int LOGN2, bool INV>
+__global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+                                                         const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  unsigned v, tile;
+  pm_decode(s, n1 / T::R, v, tile);
+  const unsigned m = s.mod(v);
+  const uint64_t q = mcs[m].q;
+  const unsigned row0 = tile * T::R;
+  const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
+  uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
+  const size_t toff = (size_t)m << (logn + 1);
+  if (q < F64_QMAX) {
+    const ArF64 ar{(double)q, 1.0 / (double)q, (INV ? tw.invd : tw.fwdd) + toff};
+    rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0);
+  } else {
+    const ArInt ar{q, (INV ? tw.inv : tw.fwd) + toff};
+    rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0);
   }
 }
 
@@ -816,7 +969,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
 {
   const unsigned logn = G.logn, n = G.n;
   const unsigned blocks = s.count * (n / 4096);
-  const Tw2 tw{G.tw2, G.itw2};
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const double pass_bytes = 16.0 * n * s.count;
   static const bool rows8 = !getenv("GPQHE_NTT2ROWS");
   if (!inverse) {
@@ -1939,7 +2092,7 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
   const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
                d01_stride = 2 * (size_t)lvl * n, acc_stride = 2 * (size_t)nm * n;
-  const Tw2 tw{G.tw2, G.itw2};
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned tiles = n / 4096;
   const double own = (double)G.alpha * ndig;  // digit slots not converted (approx. for partial digits)
   {
@@ -1980,7 +2133,7 @@ static void tensor_rows_launch(uint64_t *d01, uint64_t *d2r, const uint64_t *a, 
                                size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab)
 {
   ProfScope ps(KC_TENSOR, 8.0 * G.n * lvl * count * 7);  // read 4 limbs, write 3 limbs
-  const Tw2 tw{G.tw2, G.itw2};
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   hipLaunchKernelGGL((tensor_rows_kernel<LOGN2>), dim3(lvl * count * (G.n / 4096)), dim3(256), 0, G.stream, d01,
                      (size_t)2 * lvl * G.n, d2r, (size_t)lvl * G.n, a, b, in_stride, in_pstride, G.logn, lvl, count,
                      tab.n2i, tw, G.dev.mc);
@@ -2431,7 +2584,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
                             const uint64_t *d01, size_t d01_pstride, unsigned npoly, unsigned lvl, DownTable &tab)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
-  const Tw2 tw{G.tw2, G.itw2};
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   {
     // reads the nd row-transformed drop limbs, writes keep column-transformed limbs
     ProfScope ps(KC_DN_COLS, 8.0 * n * npoly * (tab.nd + keep));
@@ -2541,6 +2694,22 @@ void tables_upload()
   HIP_CHECK(hipMalloc((void **)&G.itw2, 2 * nm * n * 8));
   HIP_CHECK(hipMemcpy((void *)G.tw2, f2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy((void *)G.itw2, i2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
+  // FP64 twiddles (w, w / q) for the moduli below 2^50 (others unused)
+  std::vector<double> fd(2 * nm * n), id(2 * nm * n);
+  for (size_t m = 0; m < nm; m++) {
+    const double qd = (double)G.q[m];
+    for (size_t k = 0; k < n; k++) {
+      const size_t j = m * n + k;
+      fd[2 * j] = (double)tw[j];
+      fd[2 * j + 1] = (double)tw[j] / qd;
+      id[2 * j] = (double)itw[j];
+      id[2 * j + 1] = (double)itw[j] / qd;
+    }
+  }
+  HIP_CHECK(hipMalloc((void **)&G.twd, 2 * nm * n * 8));
+  HIP_CHECK(hipMalloc((void **)&G.itwd, 2 * nm * n * 8));
+  HIP_CHECK(hipMemcpy((void *)G.twd, fd.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy((void *)G.itwd, id.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
 }
 
 void tables_free()
@@ -2552,7 +2721,10 @@ void tables_free()
   HIP_CHECK(hipFree(G.dev.itwp));
   HIP_CHECK(hipFree((void *)G.tw2));
   HIP_CHECK(hipFree((void *)G.itw2));
+  HIP_CHECK(hipFree((void *)G.twd));
+  HIP_CHECK(hipFree((void *)G.itwd));
   G.tw2 = G.itw2 = nullptr;
+  G.twd = G.itwd = nullptr;
   G.dev = DevTables{};
   for (auto &kv : g_up) {
     HIP_CHECK(hipFree(kv.second.dig));
