@@ -535,7 +535,8 @@ __device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double 
 struct ArInt {
   using V = uint64_t;
   uint64_t q;
-  const uint64_t *tw;  // this modulus' (w, w') pairs
+  const uint64_t *tw;   // this modulus' forward (w, w') pairs
+  const uint64_t *itw;  // and inverse
   __device__ static V load(uint64_t x) { return x; }
   __device__ uint64_t canon(V x) const { return canon4(x, q, 2 * q); }  // x < 4q
   __device__ static uint64_t bits(V x) { return x; }
@@ -543,7 +544,7 @@ struct ArInt {
   template <int LE>
   __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const { fwd_stages<LE>(x, tw, bb, log_thi, q); }
   template <int LE>
-  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, tw, bb, log_tlo, q); }
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, itw, bb, log_tlo, q); }
   // canonical x w for a constant w < q (Shoup pair)
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
 };
@@ -551,7 +552,8 @@ struct ArInt {
 struct ArF64 {
   using V = double;
   double q, qinv;
-  const double *tw;  // this modulus' (w, w / q) pairs
+  const double *tw;   // this modulus' forward (w, w / q) pairs
+  const double *itw;  // and inverse
   __device__ static V load(uint64_t x) { return (double)x; }
   __device__ uint64_t canon(V x) const
   {
@@ -569,7 +571,7 @@ struct ArF64 {
   template <int LE>
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
-    inv_stages_f<LE>(x, tw, bb, log_tlo, q, qinv);
+    inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv);
   }
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
   {
@@ -579,6 +581,17 @@ struct ArF64 {
 };
 
 constexpr uint64_t F64_QMAX = 1ull << 50;  // ArF64 applies to moduli below this
+
+// Run f with the arithmetic policy of modulus index m (q = its prime).
+template <class F>
+__device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
+{
+  const size_t o = (size_t)m << (logn + 1);
+  if (q < F64_QMAX && tw.fwdd)
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+  else
+    f(ArInt{q, tw.fwd + o, tw.inv + o});
+}
 
 // Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
 // B reads 16 consecutive columns per thread at a 16-column lane stride; the
@@ -682,14 +695,7 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, un
     sw = post ? post[2 * (v % s.per)] : mc.ninv;
     swp = post ? post[2 * (v % s.per) + 1] : mc.ninvp;
   }
-  const size_t toff = (size_t)m << (logn + 1);
-  if (mc.q < F64_QMAX) {
-    const ArF64 ar{(double)mc.q, 1.0 / (double)mc.q, (INV ? tw.invd : tw.fwdd) + toff};
-    cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp);
-  } else {
-    const ArInt ar{mc.q, (INV ? tw.inv : tw.fwd) + toff};
-    cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp);
-  }
+  with_arith(mc.q, m, logn, tw, [&](const auto &ar) { cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp); });
 }
 
 // Row pass: tile = R rows x N2 columns (R N2 = 4096).
@@ -954,14 +960,7 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
   const unsigned row0 = tile * T::R;
   const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
   uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
-  const size_t toff = (size_t)m << (logn + 1);
-  if (q < F64_QMAX) {
-    const ArF64 ar{(double)q, 1.0 / (double)q, (INV ? tw.invd : tw.fwdd) + toff};
-    rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0);
-  } else {
-    const ArInt ar{q, (INV ? tw.inv : tw.fwd) + toff};
-    rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0);
-  }
+  with_arith(q, m, logn, tw, [&](const auto &ar) { rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0); });
 }
 
 template <int LOGT1, int LOGN2>
@@ -1914,20 +1913,23 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
   }
 }
 
-// Key layout used by ks_rows: inside every 4096-element row tile (R rows x N2),
-// element rr N2 + 16 g + k sits at k 256 + rr (N2 / 16) + g, i.e. in the
-// register ownership of round B, so every thread's 16 key words are loaded
-// coalesced.
-__device__ __forceinline__ unsigned own_perm(unsigned idx, unsigned logn2)
+// Key layout used by ks_rows: inside every 2048-element row tile, element
+// 8 th + k (the 8 consecutive residues thread th owns after the row pass)
+// sits at k 256 + th, so each thread's key words are loaded coalesced.
+__device__ __forceinline__ unsigned own_perm(unsigned idx)
 {
-  const unsigned tile = idx >> 12, e = idx & 4095;
-  const unsigned rr = e >> logn2, c = e & ((1u << logn2) - 1), g = c >> 4, k = c & 15;
-  const unsigned th = (rr << (logn2 - 4)) + g;
-  return (tile << 12) + (k << 8) + th;
+  const unsigned e = idx & 2047;
+  return (idx & ~2047u) + ((e & 7) << 8) + (e >> 3);
 }
 
+// Relinearization inner product with the forward row pass fused in front:
+// for (basis slot t, 2048-element row tile, ciphertext p) and each digit j,
+// the column-transformed limb T1[j][t] (own digit: the NTT-form d2 limb) gets
+// its row pass and is multiplied into the Montgomery-form key; both
+// accumulators stay in registers.  P (d0, d1) is added on [p_lo, lvl); limbs
+// t >= drop_lo leave after the inverse row pass (input of dn_cols).
 template <int LOGN2>
-__global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
+__global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
                                                        size_t d2_stride, const uint64_t *d01, size_t d01_stride,
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
@@ -1935,11 +1937,10 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
                                                        unsigned p_lo, unsigned drop_lo, int own_rowform, Tw2 tw,
                                                        const ModConst *mcs)
 {
-  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
-  __shared__ uint64_t acc1[16 * 256];  // a1 accumulators, thread-private slots k 256 + th
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
   const unsigned n1 = 1u << (logn - LOGN2);
-  const unsigned tiles = n1 / R;
+  const unsigned tiles = n1 / T::R;
   unsigned grp, p;  // group = (basis slot t, tile) on one XCD; members = ciphertexts
   if (!xcd_group(count, nm * tiles, grp, p))
     return;
@@ -1947,140 +1948,112 @@ __global__ void __launch_bounds__(256, 2) ks_rows_kernel(const uint64_t *T1, siz
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
   const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * R;
+  const unsigned row0 = tile * T::R;
   const size_t toff = (size_t)row0 << LOGN2;  // tile offset inside a limb
-  const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
-  const int th = threadIdx.x;
-  const int g = th % (N2 / 16), rr = th / (N2 / 16);
-  // natural-layout tile <-> round-B ownership through the swizzled LDS tile
-  auto load_own = [&](const uint64_t *src, uint64_t (&r)[16]) {
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
+  // natural-layout tile <-> ownership (8 th + k) through the swizzled LDS tile
+  auto load_own = [&](const uint64_t *src, uint64_t (&r)[8]) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < 8; i++) {
       const int e = th + 256 * i;
-      lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = src[e];
+      lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = src[e];
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = lds[rr * SP + rswz(16 * g + k)];
+    for (int k = 0; k < 8; k++)
+      r[k] = lds[T::at(row, 8 * h + k)];
   };
-  auto store_own = [&](uint64_t *dst, const uint64_t (&r)[16]) {
+  auto store_own = [&](uint64_t *dst, const uint64_t (&r)[8]) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      lds[rr * SP + rswz(16 * g + k)] = r[k];
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, 8 * h + k)] = r[k];
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < 8; i++) {
       const int e = th + 256 * i;
-      dst[e] = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
+      dst[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
     }
   };
   // 64-bit lazy accumulators in [0, 2q): each product v * evk_mont is reduced
   // by a REDC without its final correction (v, evk < q gives a result < 2q)
-  uint64_t a0[16];
+  uint64_t a0[8], a1[8];
 #pragma unroll
-  for (int k = 0; k < 16; k++)
-    a0[k] = acc1[256 * k + threadIdx.x] = 0;
+  for (int k = 0; k < 8; k++)
+    a0[k] = a1[k] = 0;
   auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
     const uint64_t lo = v * w, hi = mulhi64(v, w);
     const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
     a = lazy_lt2q(a + r, q2);
   };
-  for (unsigned j = 0; j < ndig; j++) {
-    const uint64_t *eb = evkm + (((size_t)(2 * j) * nmod + m) << logn) + toff + th;
-    const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
-    uint64_t r[16];
-    const bool own = t < lvl && t / alpha == j;
-    if (own && !own_rowform) {
-      load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, r);  // own digit: NTT-form d2
-    } else {
-      // converted limb from ks_cols, or (row form) the own d2 limb's column intermediate
-      const uint64_t *x = own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
-                              : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
-      __syncthreads();
+  with_arith(q, m, logn, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    using V = typename A::V;
+    for (unsigned j = 0; j < ndig; j++) {
+      const uint64_t *eb = evkm + (((size_t)(2 * j) * nmod + m) << logn) + toff + th;
+      const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
+      uint64_t v[8];
+      const bool own = t < lvl && t / alpha == j;
+      if (own && !own_rowform) {
+        load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, v);  // own digit: NTT-form d2
+      } else {
+        // converted limb from ks_cols, or (row form) the own d2 limb's column intermediate
+        const uint64_t *x = own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
+                                : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+        V r[8];
 #pragma unroll
-      for (int it = 0; it < R / 16; it++) {
-        const int item = th + 256 * it, l = item % 16, ra = item / 16;
-        uint64_t v[EA];
-#pragma unroll
-        for (int k = 0; k < EA; k++)
-          v[k] = x[(ra << LOGN2) + l + 16 * k];
-        fwd_stages<LEA>(v, tw2, (uint64_t)(n1 + row0 + ra) << LOGN2, LOGN2 - 1, q);
-#pragma unroll
-        for (int k = 0; k < EA; k++)
-          lds[ra * SP + rswz(l + 16 * k)] = v[k];
+        for (int k = 0; k < 8; k++)
+          r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+        __syncthreads();
+        rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
       }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        mac(a0[k], v[k], eb[256 * k]);
+        mac(a1[k], v[k], ea[256 * k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+      a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+    }
+    if (t < lvl && t >= p_lo) {
+      uint64_t c[8];
+      const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
+      load_own(c0, c);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        a0[k] = add_mod(a0[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
+      load_own(c0 + ((size_t)lvl << logn), c);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        a1[k] = add_mod(a1[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
+    }
+    uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
+    uint64_t *o1 = o0 + ((size_t)nm << logn);
+    if (t < drop_lo) {
+      store_own(o0, a0);
+      store_own(o1, a1);
+      return;
+    }
+    // limb dropped by the following ModDown: inverse row pass here (the
+    // registers hold round C's ownership); dn_cols finishes the INTT
+    auto inv_store = [&](uint64_t *dst, const uint64_t (&a)[8]) {
+      V r[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        r[k] = A::load(a[k]);
       __syncthreads();
+      rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
 #pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = lds[rr * SP + rswz(16 * g + k)];
-      fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = canon4(r[k], q, q2);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      mac(a0[k], r[k], eb[256 * k]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-      uint64_t a = acc1[256 * k + th];
-      mac(a, r[k], ea[256 * k]);
-      acc1[256 * k + th] = a;
-    }
-  }
-  uint64_t a1[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
-    a1[k] = acc1[256 * k + th];
-    a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
-  }
-  if (t < lvl && t >= p_lo) {
-    uint64_t c[16];
-    const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
-    load_own(c0, c);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      a0[k] = add_mod(a0[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
-    load_own(c0 + ((size_t)lvl << logn), c);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      a1[k] = add_mod(a1[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
-  }
-  uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
-  if (t < drop_lo) {
-    store_own(o0, a0);
-    store_own(o0 + ((size_t)nm << logn), a1);
-    return;
-  }
-  // limb dropped by the following ModDown: apply the inverse row pass here (the
-  // registers already hold round B's ownership); dn_cols finishes the INTT
-  const uint64_t *itw2 = tw.inv + ((size_t)m << (logn + 1));
-  auto inv_rows_store = [&](uint64_t *dst, uint64_t (&r)[16]) {
-    inv_stages<4>(r, itw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      lds[rr * SP + rswz(16 * g + k)] = r[k];
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < R / 16; it++) {
-      const int item = th + 256 * it, l = item % 16, ra = item / 16;
-      uint64_t v[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        v[k] = lds[ra * SP + rswz(l + 16 * k)];
-      inv_stages<LEA>(v, itw2, (uint64_t)(n1 + row0 + ra) << LOGN2, 4, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        dst[(ra << LOGN2) + l + 16 * k] = canon4(v[k], q, q2);
-    }
-  };
-  inv_rows_store(o0, a0);
-  inv_rows_store(o0 + ((size_t)nm << logn), a1);
+      for (int k = 0; k < 8; k++)
+        dst[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+    };
+    inv_store(o0, a0);
+    inv_store(o1, a1);
+  });
 }
 
 template <int LOGT1, int LOGN2>
@@ -2122,7 +2095,7 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key once, writes acc
   ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
                                                        2 * nm) + 2.0 * ndig * nm));
-  hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * tiles)), dim3(256), 0, G.stream, T1,
+  hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream, T1,
                      t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
                      ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
@@ -2197,7 +2170,7 @@ __global__ void to_mont_kernel(uint64_t *out, const uint64_t *in, unsigned logn,
   const unsigned limb = blockIdx.y % nmod;
   const size_t base = (size_t)blockIdx.y << logn;
   const ModConst m = mc[limb];
-  const size_t dst = logn2 ? own_perm((unsigned)k, logn2) : k;
+  const size_t dst = logn2 ? own_perm((unsigned)k) : k;
   out[base + dst] = mul_mod(in[base + k], m.r64, m);
 }
 
@@ -2706,6 +2679,8 @@ void tables_upload()
       id[2 * j + 1] = (double)itw[j] / qd;
     }
   }
+  if (getenv("GPQHE_NO_F64"))  // integer butterflies everywhere (A/B switch)
+    return;
   HIP_CHECK(hipMalloc((void **)&G.twd, 2 * nm * n * 8));
   HIP_CHECK(hipMalloc((void **)&G.itwd, 2 * nm * n * 8));
   HIP_CHECK(hipMemcpy((void *)G.twd, fd.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
