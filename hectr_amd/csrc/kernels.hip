@@ -2056,6 +2056,177 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
   });
 }
 
+// Key-stationary variant for two-digit keys (the bench's dnum = 2): a block
+// owns (basis slot t, row tile) and a run of ciphertexts [p0, p1).  The key
+// words of both digits stay in registers for the whole run (no per-ciphertext
+// key traffic), and the next ciphertext's two input tiles are prefetched into
+// registers while the current one is transformed and accumulated, so one load
+// latency is exposed per block instead of several per ciphertext.
+template <int LOGN2>
+__global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
+                                                           size_t d2_stride, const uint64_t *d01, size_t d01_stride,
+                                                           const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
+                                                           unsigned logn, unsigned lvl, unsigned L, unsigned nm,
+                                                           unsigned nmod, unsigned alpha, unsigned count,
+                                                           unsigned cpb, unsigned members, unsigned p_lo,
+                                                           unsigned drop_lo, int own_rowform, Tw2 tw,
+                                                           const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / T::R;
+  unsigned grp, mi;  // group = (basis slot t, tile) on one XCD; members = ciphertext runs
+  if (!xcd_group(members, nm * tiles, grp, mi))
+    return;
+  const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
+  if (p0 >= p1)
+    return;
+  const unsigned t = grp / tiles, tile = grp % tiles;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * T::R;
+  const size_t toff = (size_t)row0 << LOGN2;
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
+  // digit j's input for ciphertext p: own digit -> the NTT-form d2 limb
+  // (natural layout, transposed through LDS), else T1[j][t] (row pass input)
+  const bool own0 = t < lvl && t / alpha == 0, own1 = t < lvl && t / alpha == 1;
+  const bool nat0 = own0 && !own_rowform, nat1 = own1 && !own_rowform;
+  auto src = [&](unsigned j, unsigned p) -> const uint64_t * {
+    const bool own = j ? own1 : own0;
+    return own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
+               : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+  };
+  auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
+    const uint64_t *s_ = src(j, p);
+    if (j ? nat1 : nat0) {
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        x[i] = s_[th + 256 * i];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        x[k] = s_[(row << LOGN2) + l + T::TA * k];
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      kl[c][256 * k + th] = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
+  uint64_t xn[2][8];
+  fetch(xn[0], 0, p0);
+  fetch(xn[1], 1, p0);
+  auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
+    const uint64_t lo = v * w, hi = mulhi64(v, w);
+    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
+    a = lazy_lt2q(a + r, q2);
+  };
+  with_arith(q, m, logn, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    using V = typename A::V;
+    for (unsigned p = p0; p < p1; p++) {
+      uint64_t a0[8], a1[8];
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        uint64_t v[8];
+        __syncthreads();  // the previous phase has finished with the LDS tile
+        if (j ? nat1 : nat0) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const int e = th + 256 * i;
+            lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = xn[j][i];
+          }
+          if (p + 1 < p1)
+            fetch(xn[j], j, p + 1);  // prefetch: in flight during the rest of this ciphertext
+          __syncthreads();
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            v[k] = lds[T::at(row, 8 * h + k)];
+        } else {
+          V r[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            r[k] = A::load(xn[j][k]);
+          if (p + 1 < p1)
+            fetch(xn[j], j, p + 1);
+          rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (j == 0) {
+            a0[k] = a1[k] = 0;
+          }
+          mac(a0[k], v[k], kl[2 * j][256 * k + th]);
+          mac(a1[k], v[k], kl[2 * j + 1][256 * k + th]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+        a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+      }
+      if (t < lvl && t >= p_lo) {
+        const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const int e = th + 256 * i;
+            lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = c0[((size_t)half * lvl << logn) + e];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const uint64_t c = mul_shoup(lds[T::at(row, 8 * h + k)], mc.pmod, mc.pmodp, q);
+            if (half)
+              a1[k] = add_mod(a1[k], c, q);
+            else
+              a0[k] = add_mod(a0[k], c, q);
+          }
+        }
+      }
+      uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
+      uint64_t *o1 = o0 + ((size_t)nm << logn);
+      if (t < drop_lo) {
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          __syncthreads();
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            lds[T::at(row, 8 * h + k)] = half ? a1[k] : a0[k];
+          __syncthreads();
+          uint64_t *dst = half ? o1 : o0;
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const int e = th + 256 * i;
+            dst[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
+          }
+        }
+      } else {
+        // limb dropped by the following ModDown: inverse row pass (dn_cols
+        // finishes the INTT)
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          V r[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            r[k] = A::load(half ? a1[k] : a0[k]);
+          __syncthreads();
+          rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
+          uint64_t *dst = half ? o1 : o0;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            dst[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+        }
+      }
+    }
+  });
+}
+
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
                             const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
@@ -2095,9 +2266,19 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key once, writes acc
   ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
                                                        2 * nm) + 2.0 * ndig * nm));
-  hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream, T1,
-                     t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod,
-                     ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+  if (ndig == 2 && !getenv("GPQHE_KSROWS_STREAM")) {
+    // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
+    const unsigned groups = nm * (n / 2048);
+    const unsigned members = std::max(1u, std::min(count, (4 * 256 + groups - 1) / groups));
+    const unsigned cpb = (count + members - 1) / members;
+    hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
+                       t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
+                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+  } else {
+    hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
+                       T1, t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
+                       G.nmod, ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
