@@ -1880,36 +1880,40 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
 #pragma unroll
     for (int i = 0; i < 4; i++)
       cc[i] = i < (int)na ? tab.c[((size_t)j * 8 + i) * nm + t] : 0;
-    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
     uint64_t *buf = lds[u & 1];
-#pragma unroll
-    for (int it = 0; it < IT; it++) {
-      const int item = th + 256 * it, c = item % C, l = item / C;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++) {
-        unsigned __int128 acc = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          acc += (unsigned __int128)y[it][i][k] * cc[i];
-        r[k] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc);
-      }
-      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        buf[(l + 16 * k) * CP + c] = r[k];
-    }
-    __syncthreads();
     uint64_t *out = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + (size_t)tile * C;
-    const int c = th % C, g = th / C;
-    uint64_t r[16];
+    with_arith(q, m, logn, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      using V = typename A::V;
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = buf[(16 * g + k) * CP + c];
-    fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+      for (int it = 0; it < IT; it++) {
+        const int item = th + 256 * it, c = item % C, l = item / C;
+        V r[EA];
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+        for (int k = 0; k < EA; k++) {
+          unsigned __int128 acc = 0;
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            acc += (unsigned __int128)y[it][i][k] * cc[i];
+          r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+        }
+        ar.template fwd<LEA>(r, T, LOGT - 1);
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          buf[(l + 16 * k) * CP + c] = A::bits(r[k]);
+      }
+      __syncthreads();
+      const int c = th % C, g = th / C;
+      V r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = A::unbits(buf[(16 * g + k) * CP + c]);
+      ar.template fwd<4>(r, T + 16 * g, 3);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+    });
+    (void)q2;
   }
 }
 
@@ -2580,41 +2584,43 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
     if (d >= (int)nd)
       break;
     const unsigned md = basis_mod(keep + d, lvl, L);
-    const uint64_t qd = mcs[md].q;
-    const uint64_t *itw2 = tw.inv + ((size_t)md << (logn + 1));
     const uint64_t w = tab.ysc[2 * d], wp = tab.ysc[2 * d + 1];
     const uint64_t *src = yb + ((size_t)d << logn);
     if (d)
       __syncthreads();
-    {
-      const int c = th % C, g = th / C;
-      uint64_t r[16];
+    with_arith(mcs[md].q, md, logn, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      using V = typename A::V;
+      {
+        const int c = th % C, g = th / C;
+        V r[16];
 #pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = src[(size_t)(16 * g + k) * n2 + c];
-      inv_stages<4>(r, itw2, T + 16 * g, 0, qd);
+        for (int k = 0; k < 16; k++)
+          r[k] = A::load(src[(size_t)(16 * g + k) * n2 + c]);
+        ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
-      for (int k = 0; k < 16; k++)
-        lds[(16 * g + k) * CP + c] = r[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < IT; it++) {
-      const int item = th + 256 * it, c = item % C, l = item / C;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = lds[(l + 16 * k) * CP + c];
-      inv_stages<LEA>(r, itw2, T, 4, qd);
-#pragma unroll
-      for (int k = 0; k < EA; k++) {
-        const uint64_t v = mul_shoup(r[k], w, wp, qd);
-        if (d < 4)
-          y[it][d < 4 ? d : 0][k] = v;
-        else if constexpr (X5)
-          y5[(it * EA + k) * 256 + th] = v;
+        for (int k = 0; k < 16; k++)
+          lds[(16 * g + k) * CP + c] = A::bits(r[k]);
       }
-    }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < IT; it++) {
+        const int item = th + 256 * it, c = item % C, l = item / C;
+        V r[EA];
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          r[k] = A::unbits(lds[(l + 16 * k) * CP + c]);
+        ar.template inv<LEA>(r, T, 4);
+#pragma unroll
+        for (int k = 0; k < EA; k++) {
+          const uint64_t v = ar.mulc(r[k], w, wp);
+          if (d < 4)
+            y[it][d < 4 ? d : 0][k] = v;
+          else if constexpr (X5)
+            y5[(it * EA + k) * 256 + th] = v;
+        }
+      }
+    });
   }
 #pragma unroll
   for (int d = 0; d < 4; d++)
@@ -2636,52 +2642,59 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 #pragma unroll
     for (int d = 0; d < 5; d++)
       cc[d] = d < (int)nd ? tab.c[(size_t)d * keep + t] : 0;
-    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
     if (u)
       __syncthreads();  // the previous target's round B has read the tile
-#pragma unroll
-    for (int it = 0; it < IT; it++) {
-      const int item = th + 256 * it, c = item % C, l = item / C;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++) {
-        unsigned __int128 acc = 0;
-#pragma unroll
-        for (int d = 0; d < 4; d++)
-          acc += (unsigned __int128)y[it][d][k] * cc[d];
-        if constexpr (X5)
-          acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
-        r[k] = redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc);
-      }
-      fwd_stages<LEA>(r, tw2, T, LOGT - 1, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        lds[(l + 16 * k) * CP + c] = r[k];
-    }
-    __syncthreads();
     uint64_t *out = conv + (((size_t)p * keep + t) << logn) + (size_t)tile * C;
-    const int c = th % C, g = th / C;
-    uint64_t r[16];
+    with_arith(q, m, logn, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      using V = typename A::V;
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = lds[(16 * g + k) * CP + c];
-    fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+      for (int it = 0; it < IT; it++) {
+        const int item = th + 256 * it, c = item % C, l = item / C;
+        V r[EA];
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+        for (int k = 0; k < EA; k++) {
+          unsigned __int128 acc = 0;
+#pragma unroll
+          for (int d = 0; d < 4; d++)
+            acc += (unsigned __int128)y[it][d][k] * cc[d];
+          if constexpr (X5)
+            acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
+          r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+        }
+        ar.template fwd<LEA>(r, T, LOGT - 1);
+#pragma unroll
+        for (int k = 0; k < EA; k++)
+          lds[(l + 16 * k) * CP + c] = A::bits(r[k]);
+      }
+      __syncthreads();
+      const int c = th % C, g = th / C;
+      V r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = A::unbits(lds[(16 * g + k) * CP + c]);
+      ar.template fwd<4>(r, T + 16 * g, 3);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+    });
+    (void)q2;
   }
 }
 
+// Forward row pass of conv on 8-element row tiles with the combine as its
+// epilogue.  The epilogue operands (X_t, d_{0,1,t}) are fetched at kernel
+// start so their latency overlaps the row pass.
 template <int LOGN2>
 __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint64_t *out, size_t out_pstride,
                                                        const uint64_t *X, size_t x_pstride, const uint64_t *d01,
                                                        size_t d01_pstride, unsigned logn, unsigned lvl, unsigned L,
                                                        unsigned npoly, DownTable tab, Tw2 tw, const ModConst *mcs)
 {
-  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
   const unsigned n1 = 1u << (logn - LOGN2);
-  const unsigned tiles = n1 / R;
+  const unsigned tiles = n1 / T::R;
   const unsigned keep = tab.keep;
   unsigned grp, p;  // group = (target t, tile) on one XCD; members = polynomials
   if (!xcd_group(npoly, keep * tiles, grp, p))
@@ -2689,47 +2702,41 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   const unsigned t = grp / tiles, tile = grp % tiles;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
-  const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * R;
+  const uint64_t q = mc.q;
+  const unsigned row0 = tile * T::R;
   const size_t toff = ((size_t)t << logn) + ((size_t)row0 << LOGN2);
   const uint64_t *x = conv + (((size_t)p * keep) << logn) + toff;
-  const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
-  const int th = threadIdx.x;
-#pragma unroll
-  for (int it = 0; it < R / 16; it++) {
-    const int item = th + 256 * it, l = item % 16, rr = item / 16;
-    uint64_t r[EA];
-#pragma unroll
-    for (int k = 0; k < EA; k++)
-      r[k] = x[(rr << LOGN2) + l + 16 * k];
-    fwd_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, LOGN2 - 1, q);
-#pragma unroll
-    for (int k = 0; k < EA; k++)
-      lds[rr * SP + rswz(l + 16 * k)] = r[k];
-  }
-  __syncthreads();
-  {
-    const int g = th % (N2 / 16), rr = th / (N2 / 16);
-    uint64_t r[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = lds[rr * SP + rswz(16 * g + k)];
-    fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      lds[rr * SP + rswz(16 * g + k)] = canon4(r[k], q, q2);
-  }
-  __syncthreads();
-  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], f = tab.fin[2 * t], fp = tab.fin[2 * t + 1];
   const uint64_t *xs = X + p * x_pstride + toff;
   const uint64_t *ds = d01 + p * d01_pstride + toff;
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
+  uint64_t xv[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    xv[i] = xs[th + 256 * i];
+    dv[i] = ds[th + 256 * i];
+  }
+  uint64_t cv[8];
+  with_arith(q, m, logn, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    typename A::V r[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+    rows8_fwd<LOGN2>(r, cv, lds, ar, n1 + row0);
+  });
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    lds[T::at(row, 8 * h + k)] = cv[k];
+  __syncthreads();
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], f = tab.fin[2 * t], fp = tab.fin[2 * t + 1];
   uint64_t *o = out + p * out_pstride + toff;
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
+  for (int i = 0; i < 8; i++) {
     const int e = th + 256 * i;
-    const uint64_t cv = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
-    const uint64_t v = mul_shoup(sub_mod(xs[e], cv, q), dinv, dinvp, q);
-    o[e] = add_mod(v, mul_shoup(ds[e], f, fp, q), q);
+    const uint64_t c = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
+    const uint64_t v = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
+    o[e] = add_mod(v, mul_shoup(dv[i], f, fp, q), q);
   }
 }
 
@@ -2753,7 +2760,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
   }
   // reads conv, X and d01 keep limbs, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
-  hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * tiles)), dim3(256), 0, G.stream, conv,
+  hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
                      out, out_pstride, X, x_pstride, d01, d01_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
