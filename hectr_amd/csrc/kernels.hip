@@ -2074,7 +2074,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
                                                            unsigned nmod, unsigned alpha, unsigned count,
                                                            unsigned cpb, unsigned members, unsigned p_lo,
                                                            unsigned drop_lo, int own_rowform, Tw2 tw,
-                                                           const ModConst *mcs)
+                                                           const ModConst *mcs, int ablate)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
@@ -2156,15 +2156,26 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
             r[k] = A::load(xn[j][k]);
           if (p + 1 < p1)
             fetch(xn[j], j, p + 1);
-          rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
+          if (ablate & 1) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+              v[k] = A::bits(r[k]);
+          } else {
+            rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
+          }
         }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (j == 0) {
             a0[k] = a1[k] = 0;
           }
-          mac(a0[k], v[k], kl[2 * j][256 * k + th]);
-          mac(a1[k], v[k], kl[2 * j + 1][256 * k + th]);
+          if (ablate & 2) {
+            a0[k] += v[k];
+            a1[k] ^= v[k];
+          } else {
+            mac(a0[k], v[k], kl[2 * j][256 * k + th]);
+            mac(a1[k], v[k], kl[2 * j + 1][256 * k + th]);
+          }
         }
       }
 #pragma unroll
@@ -2195,7 +2206,10 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
       }
       uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
       uint64_t *o1 = o0 + ((size_t)nm << logn);
-      if (t < drop_lo) {
+      if (ablate & 4) {
+        if (a0[0] == 0x1234567 && a1[1] == 0x89)  // keeps the values live
+          o0[th] = a0[2] + a1[3];
+      } else if (t < drop_lo || (ablate & 8)) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           __syncthreads();
@@ -2230,6 +2244,11 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
     }
   });
 }
+
+// Debug ablation mask for timing studies (GPQHE_ABLATE; results are wrong
+// when set): 1 skip row NTT, 2 skip key MAC, 4 skip acc stores, 8 skip the
+// inverse row pass of dropped limbs.
+static const int g_ablate = getenv("GPQHE_ABLATE") ? atoi(getenv("GPQHE_ABLATE")) : 0;
 
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
@@ -2277,7 +2296,8 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
                        t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc,
+                       g_ablate);
   } else {
     hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
                        T1, t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
