@@ -45,6 +45,7 @@ def parse():
                     help="key-switch digits (2: fastest measured at L=8, see DESIGN.md; L: one limb per digit)")
     ap.add_argument("--nspecial", type=int, default=0, help="special primes K (default: enough for P > digit)")
     ap.add_argument("--p-bits", type=int, default=60, help="special prime size in bits")
+    ap.add_argument("--q0-bits", type=int, default=60, help="first prime size in bits")
     ap.add_argument("--no-cstr", action="store_true", help="skip the encrypted CSTR loop (config 4)")
     ap.add_argument("--cstr-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -71,9 +72,9 @@ def main():
     L, logn, B = args.nlimbs, args.logn, args.batch
     n = 1 << logn
     dnum = args.dnum or L
-    K = args.nspecial or special_primes(L, dnum, p_bits=args.p_bits)
+    K = args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits, p_bits=args.p_bits)
     eng = Engine.product()
-    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=60, qi_bits=50,
+    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=args.q0_bits, qi_bits=50,
                     p_bits=args.p_bits, seed=1000 + rank)
     stream = torch.cuda.Stream()
     eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
@@ -270,8 +271,9 @@ def cpu_baseline(args, logn, L, dnum):
     from hectr_amd.gpqhe import Engine
     threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
     ora = Engine.oracle()
-    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=60, qi_bits=50, p_bits=args.p_bits, seed=7,
-                    nspecial=args.nspecial or special_primes(L, dnum, p_bits=args.p_bits))
+    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=args.q0_bits, qi_bits=50, p_bits=args.p_bits,
+                    seed=7, nspecial=args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits,
+                                                                     p_bits=args.p_bits))
     pk, sk, rlk = ora.pk(), ora.sk(), ora.evk()
     ora.keypair(pk, sk)
     ora.genrlk(rlk, sk)

@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(TPB) ntt_rows_kernel(LimbSet s, unsigned logn,
 struct Tw2 {
   const uint64_t *fwd;  // [nmod][n][2] (w, floor(w 2^64 / q))
   const uint64_t *inv;
-  const double *fwdd;   // [nmod][n][2] (w, w / q) as doubles (moduli < 2^50)
+  const double *fwdd;   // [nmod][n][2] (w, w / q) as doubles (moduli < 2^51)
   const double *invd;
 };
 
@@ -462,15 +462,15 @@ __device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_
 }
 
 // ---------------------------------------------------------------------------
-// FP64 butterflies for moduli q < 2^50 (the FP64 pipe is full rate on gfx950
+// FP64 butterflies for moduli q < 2^51 (the FP64 pipe is full rate on gfx950
 // and twice as fast as 64-bit integer Shoup per butterfly, scripts/ubench_bfly).
 // Values are signed doubles holding exact integers:
 //   mulmod: h = fl(y w), l = fma(y, w, -h) (exact), qt = rint(y fl(w/q)),
-//           T = fma(-qt, q, h) + l = y w - qt q exactly.  With |y| <= 1.5 q,
-//           |y w / q - qt| <= 1/2 + 1.5 q 2^-52 < 0.875, so |T| < 0.875 q.
+//           T = fma(-qt, q, h) + l = y w - qt q exactly.  The quotient error
+//           is below 1/2 + |y| 2^-52, so for |y| <= 2q < 2^52 |T| < 1.5 q.
 //   red:    x - rint(x fl(1/q)) q, |result| <= q/2 (+ negligible).
-// CT: X = red(x[k]), T = mulmod(x[k+h]); outputs X +- T, |.| < 1.375 q.
-// GS: outputs red(U + V) and mulmod(U - V) with |U|, |V| <= q.
+// CT: X = red(x[k]), T = mulmod(x[k+h]); outputs X +- T, |.| < 2q.
+// GS: outputs red(U + V) and mulmod(U - V) with |U - V| < 2q.
 // Every intermediate is an integer below 2^53, so the residues are exact and
 // the canonical outputs equal the integer path's bit for bit.
 // ---------------------------------------------------------------------------
@@ -531,7 +531,7 @@ __device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double 
 }
 
 // Arithmetic policies: the NTT kernels are written once against these.  Both
-// read and write canonical u64 residues; ArF64 requires q < 2^50.
+// read and write canonical u64 residues; ArF64 requires q < 2^51.
 struct ArInt {
   using V = uint64_t;
   uint64_t q;
@@ -580,7 +580,7 @@ struct ArF64 {
   }
 };
 
-constexpr uint64_t F64_QMAX = 1ull << 50;  // ArF64 applies to moduli below this
+constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
 
 // Run f with the arithmetic policy of modulus index m (q = its prime).
 template <class F>
@@ -2875,7 +2875,7 @@ void tables_upload()
   HIP_CHECK(hipMalloc((void **)&G.itw2, 2 * nm * n * 8));
   HIP_CHECK(hipMemcpy((void *)G.tw2, f2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy((void *)G.itw2, i2.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
-  // FP64 twiddles (w, w / q) for the moduli below 2^50 (others unused)
+  // FP64 twiddles (w, w / q) for the moduli below 2^51 (others unused)
   std::vector<double> fd(2 * nm * n), id(2 * nm * n);
   for (size_t m = 0; m < nm; m++) {
     const double qd = (double)G.q[m];

@@ -84,7 +84,8 @@ __global__ void bfly_f64(uint64_t *io, const double *twd, double q, double qinv,
 
 int main()
 {
-  const uint64_t qs[] = {1125899906826241ull, 1125899906629633ull, 562949953421231ull};  // < 2^50 (not nec. prime)
+  const uint64_t qs[] = {1125899906826241ull, 1125899906629633ull, 562949953421231ull,    // < 2^50
+                         2251799813554177ull, 2251799813685119ull, 2251799813160961ull};  // < 2^51 (odd, not nec. prime)
   const size_t nth = 256 * 4096, words = nth * 16;
   uint64_t *h = (uint64_t *)malloc(words * 8), *hi = (uint64_t *)malloc(words * 8), *hf = (uint64_t *)malloc(words * 8);
   uint64_t *d;
