@@ -395,6 +395,17 @@ extern "C" void hectx_exit(void)
   if (!G.init)
     return;
   HIP_CHECK(hipStreamSynchronize(G.stream));
+  for (int s = 0; s < 2; s++)
+    if (G.lane[s]) {
+      HIP_CHECK(hipStreamSynchronize(G.lane[s]));
+      HIP_CHECK(hipStreamDestroy(G.lane[s]));
+      G.lane[s] = nullptr;
+    }
+  for (int e = 0; e < 3; e++)
+    if (G.lane_ev[e]) {
+      HIP_CHECK(hipEventDestroy(G.lane_ev[e]));
+      G.lane_ev[e] = nullptr;
+    }
   gemv_cache_clear();
   tables_free();
   pool_release_all();
@@ -807,6 +818,24 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
   k_moddown(out, out_pstride, acc.p, nm * n, 2 * count, lvl, rescale ? 1 : 0);
 }
 
+// Workspace of one pipeline lane of he_mul_rescale_batch (fused path).
+struct LaneWs {
+  uint64_t *d01, *d2, *y, *T1, *acc, *conv;
+};
+
+// mul_chunk's fused path on caller-owned workspace (no pool traffic, so it
+// may run on any stream).
+static void mul_chunk_fused(const LaneWs &w, uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
+                            size_t in_stride, size_t in_pstride, unsigned count, unsigned lvl, const he_evk_t *rlk,
+                            bool rescale)
+{
+  const unsigned nm = lvl + G.K, keep = rescale ? lvl - 1 : lvl;
+  const size_t n = G.n;
+  k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride,
+                        (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, keep, keep);
+  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, w.d01, lvl * n, w.conv);
+}
+
 static void mul_core(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk, bool rescale)
 {
   check_ctx();
@@ -980,12 +1009,65 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const size_t budget = (size_t)2 << 30;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));
+  if (const char *e = getenv("GPQHE_CHUNK"))  // test hook: force small chunks (several lanes' worth)
+    chunk = std::max<size_t>(1, std::min<size_t>(chunk, strtoul(e, nullptr, 0)));
   const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
-  for (size_t c0 = 0; c0 < count; c0 += chunk) {
-    const unsigned cnt = (unsigned)std::min(chunk, count - c0);
-    mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n,
-              cnt, lvl, rlk, true);
+  const size_t nchunks = (count + chunk - 1) / chunk;
+  const bool lanes = nchunks >= 2 && k_ks_fused_ok() && rlk->reserved && rlk->dnum == G.dnum &&
+                     !getenv("GPQHE_UNFUSED") && !getenv("GPQHE_DN_UNFUSED") && getenv("GPQHE_LANES") &&
+                     !k_prof_on();
+  if (!lanes) {
+    for (size_t c0 = 0; c0 < count; c0 += chunk) {
+      const unsigned cnt = (unsigned)std::min(chunk, count - c0);
+      mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n,
+                cnt, lvl, rlk, true);
+    }
+    return;
   }
+  // Two pipeline lanes (HIP streams), chunks alternating, so one chunk's
+  // memory-bound kernels could share the CUs with the other's VALU-bound ones.
+  // Opt-in (GPQHE_LANES): measured no faster than one stream at N=2^16, L=8
+  // (each kernel fills the GPU by itself).  Each lane owns its workspace for
+  // the whole call (the pool is stream-ordered).
+  const unsigned keep = lvl - 1;
+  const size_t cw = chunk * n;
+  const size_t lane_words = cw * (2 * lvl + lvl + lvl + (size_t)ndig * nm + 2 * nm + 2 * keep);
+  uint64_t *wsb[2];
+  LaneWs ws[2];
+  for (int s = 0; s < 2; s++) {
+    if (!G.lane[s])
+      HIP_CHECK(hipStreamCreateWithFlags(&G.lane[s], hipStreamNonBlocking));
+    wsb[s] = (uint64_t *)pool_alloc(lane_words * 8);
+    uint64_t *q = wsb[s];
+    ws[s].d01 = q, q += cw * 2 * lvl;
+    ws[s].d2 = q, q += cw * lvl;
+    ws[s].y = q, q += cw * lvl;
+    ws[s].T1 = q, q += cw * ndig * nm;
+    ws[s].acc = q, q += cw * 2 * nm;
+    ws[s].conv = q;
+  }
+  for (int e = 0; e < 3; e++)
+    if (!G.lane_ev[e])
+      HIP_CHECK(hipEventCreateWithFlags(&G.lane_ev[e], hipEventDisableTiming));
+  const hipStream_t main = G.stream;
+  HIP_CHECK(hipEventRecord(G.lane_ev[2], main));
+  for (int s = 0; s < 2; s++)
+    HIP_CHECK(hipStreamWaitEvent(G.lane[s], G.lane_ev[2], 0));
+  size_t i = 0;
+  for (size_t c0 = 0; c0 < count; c0 += chunk, i++) {
+    const unsigned cnt = (unsigned)std::min(chunk, count - c0);
+    G.stream = G.lane[i & 1];
+    mul_chunk_fused(ws[i & 1], out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride,
+                    in_stride, lvl * n, cnt, lvl, rlk, true);
+  }
+  G.stream = main;
+  for (int s = 0; s < 2; s++) {
+    HIP_CHECK(hipEventRecord(G.lane_ev[s], G.lane[s]));
+    HIP_CHECK(hipStreamWaitEvent(main, G.lane_ev[s], 0));
+  }
+  // freed in main-stream order: later work on main runs after both lanes
+  pool_free(wsb[0]);
+  pool_free(wsb[1]);
 }
 
 static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)

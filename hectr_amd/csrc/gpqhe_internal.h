@@ -205,6 +205,8 @@ struct Context {
   const double *twd = nullptr, *itwd = nullptr;    // interleaved (w, w / q) doubles [nmod][n][2]
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;
+  hipStream_t lane[2] = {nullptr, nullptr};  // he_mul_rescale_batch pipeline lanes
+  hipEvent_t lane_ev[3] = {nullptr, nullptr, nullptr};
   int device = 0;
 };
 
@@ -277,7 +279,8 @@ void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t 
 // k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
 // must hold the inverse row pass of their NTT form; d01 poly p at d01 + p*d01_pstride
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode, const uint64_t *d01, size_t d01_pstride);
+                     unsigned lvl, int mode, const uint64_t *d01, size_t d01_pstride, uint64_t *conv_ws = nullptr);
+bool k_prof_on();
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();
 void tables_free();

@@ -91,6 +91,11 @@ struct ProfScope {
   }
 };
 
+bool k_prof_on()
+{
+  return g_prof;
+}
+
 extern "C" void gpqhe_prof_enable(int on)
 {
   g_prof = on != 0;
@@ -2292,7 +2297,8 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   if (ndig == 2 && !getenv("GPQHE_KSROWS_STREAM")) {
     // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
     const unsigned groups = nm * (n / 2048);
-    const unsigned members = std::max(1u, std::min(count, (4 * 256 + groups - 1) / groups));
+    static const unsigned want = getenv("GPQHE_KSR_MEMBERS") ? atoi(getenv("GPQHE_KSR_MEMBERS")) : 0;
+    const unsigned members = std::max(1u, std::min(count, want ? want : (6 * 256 + groups - 1) / groups));
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
                        t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
@@ -2786,14 +2792,14 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
 }
 
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode, const uint64_t *d01, size_t d01_pstride)
+                     int mode, const uint64_t *d01, size_t d01_pstride, uint64_t *conv_ws)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
   DownTable &tab = down_table(lvl, mode);
   if (tab.nd > 5)
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
-  uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
+  uint64_t *conv = conv_ws ? conv_ws : (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
   case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
   case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
@@ -2801,7 +2807,8 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
   case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^16");
   }
-  pool_free(conv);
+  if (!conv_ws)
+    pool_free(conv);
 }
 
 // Benchmark input generator (oracle: poly_fill_uniform).

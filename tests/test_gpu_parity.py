@@ -150,18 +150,24 @@ def test_ntt_batch_bitexact(oracle, product, name):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "c5"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "c5"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
-    latter also through the opt-in row-form key switch) and the config 5 op at
-    n=2^17, L=12 on 3 random-residue ciphertext pairs."""
+    latter also through the opt-in row-form key switch and through the
+    two-stream chunk pipeline: 5 pairs in chunks of 2) and the config 5 op at
+    n=2^17, L=12 on random-residue ciphertext pairs."""
     import ctypes
     import torch
+    cnt = 3
     if name.endswith("_rowform"):
         monkeypatch.setenv("GPQHE_KS_ROWFORM", "1")
         name = name[:-len("_rowform")]
+    if name.endswith("_lanes"):
+        monkeypatch.setenv("GPQHE_CHUNK", "2")
+        monkeypatch.setenv("GPQHE_LANES", "1")
+        name, cnt = name[:-len("_lanes")], 5
     init_both(oracle, product, name)
-    n, L, cnt = product.n, product.L, 3
+    n, L = product.n, product.L
     _, _, _, rlk_o = keys(oracle, rot=False)
     _, _, _, rlk_p = keys(product, rot=False)
     same(oracle, product, rlk_o, rlk_p)
