@@ -813,6 +813,51 @@ struct Row8 {
 
 // forward row pass of one tile, rounds A..C: round A input in r (the
 // thread's A elements), canonical result in out (the thread's C elements)
+// forward row pass of one tile leaving the thread's C elements lazy in r
+// (|.| < 2q for ArF64, < 4q for ArInt)
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int th = threadIdx.x, row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int l = th % T::TA;
+    ar.template fwd<3>(r, rb, LOGN2 - 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
+  }
+  __syncthreads();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
+    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
+  }
+  __syncthreads();
+  const int h = th % T::TA;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = A::unbits(lds[T::at(row, 8 * h + k)]);
+#pragma unroll
+  for (int j = 0; j < 8 / T::EC; j++) {
+    V g[T::EC];
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      g[e] = r[j * T::EC + e];
+    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      r[j * T::EC + e] = g[e];
+  }
+}
+
 template <int LOGN2, class A>
 __device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)[8], uint64_t *lds, const A &ar,
                                           uint64_t rowbase0)
@@ -1999,34 +2044,67 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
   with_arith(q, m, logn, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
     using V = typename A::V;
+    constexpr bool F = std::is_same<A, ArF64>::value;  // FP64 moduli: plain key, FP64 products
+    V f0[8], f1[8];
     for (unsigned j = 0; j < ndig; j++) {
       const uint64_t *eb = evkm + (((size_t)(2 * j) * nmod + m) << logn) + toff + th;
       const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
-      uint64_t v[8];
+      V r[8];
       const bool own = t < lvl && t / alpha == j;
       if (own && !own_rowform) {
+        uint64_t v[8];
         load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, v);  // own digit: NTT-form d2
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          r[k] = A::load(v[k]);
       } else {
         // converted limb from ks_cols, or (row form) the own d2 limb's column intermediate
         const uint64_t *x = own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
                                 : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
-        V r[8];
 #pragma unroll
         for (int k = 0; k < 8; k++)
           r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
         __syncthreads();
-        rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
+        rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
       }
+      if constexpr (F) {
+        // |accumulator| grows by < 1.5 q per digit; fold it back every 4 digits
+        const bool fold = (j & 3) == 3;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        mac(a0[k], v[k], eb[256 * k]);
-        mac(a1[k], v[k], ea[256 * k]);
+        for (int k = 0; k < 8; k++) {
+          const double wb = (double)eb[256 * k], wa = (double)ea[256 * k];
+          const double tb = f64_mulmod(r[k], wb, wb * ar.qinv, ar.q);
+          const double ta = f64_mulmod(r[k], wa, wa * ar.qinv, ar.q);
+          f0[k] = j ? f0[k] + tb : tb;
+          f1[k] = j ? f1[k] + ta : ta;
+          if (fold) {
+            f0[k] = f64_red(f0[k], ar.q, ar.qinv);
+            f1[k] = f64_red(f1[k], ar.q, ar.qinv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint64_t v = ar.canon(r[k]);
+          mac(a0[k], v, eb[256 * k]);
+          mac(a1[k], v, ea[256 * k]);
+        }
       }
     }
+    if constexpr (F) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
-      a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+      for (int k = 0; k < 8; k++) {
+        a0[k] = ar.canon(f0[k]);
+        a1[k] = ar.canon(f1[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+        a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+      }
+      (void)f0;
+      (void)f1;
     }
     if (t < lvl && t >= p_lo) {
       uint64_t c[8];
@@ -2120,11 +2198,14 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         x[k] = s_[(row << LOGN2) + l + T::TA * k];
     }
   };
+  const bool f64 = q < F64_QMAX && tw.fwdd;  // the key tile is plain for these moduli (to_mont_kernel)
 #pragma unroll
   for (int c = 0; c < 4; c++)
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      kl[c][256 * k + th] = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
+    for (int k = 0; k < 8; k++) {
+      const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
+      kl[c][256 * k + th] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
+    }
   uint64_t xn[2][8];
   fetch(xn[0], 0, p0);
   fetch(xn[1], 1, p0);
@@ -2138,9 +2219,10 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
     using V = typename A::V;
     for (unsigned p = p0; p < p1; p++) {
       uint64_t a0[8], a1[8];
+      V f0[8], f1[8];  // FP64 accumulators (|.| < 3q: two products of < 1.5q each)
 #pragma unroll
       for (int j = 0; j < 2; j++) {
-        uint64_t v[8];
+        V r[8];
         __syncthreads();  // the previous phase has finished with the LDS tile
         if (j ? nat1 : nat0) {
 #pragma unroll
@@ -2153,40 +2235,59 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
           __syncthreads();
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            v[k] = lds[T::at(row, 8 * h + k)];
+            r[k] = A::load(lds[T::at(row, 8 * h + k)]);
         } else {
-          V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
             r[k] = A::load(xn[j][k]);
           if (p + 1 < p1)
             fetch(xn[j], j, p + 1);
           if (ablate & 1) {
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-              v[k] = A::bits(r[k]);
           } else {
-            rows8_fwd<LOGN2>(r, v, lds, ar, n1 + row0);
+            rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
           }
         }
+        if constexpr (std::is_same<A, ArF64>::value) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          if (j == 0) {
-            a0[k] = a1[k] = 0;
+          for (int k = 0; k < 8; k++) {
+            const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
+            const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
+            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
+            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
+            f0[k] = j ? f0[k] + tb : tb;
+            f1[k] = j ? f1[k] + ta : ta;
           }
-          if (ablate & 2) {
-            a0[k] += v[k];
-            a1[k] ^= v[k];
-          } else {
-            mac(a0[k], v[k], kl[2 * j][256 * k + th]);
-            mac(a1[k], v[k], kl[2 * j + 1][256 * k + th]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const uint64_t v = ar.canon(r[k]);
+            if (j == 0) {
+              a0[k] = a1[k] = 0;
+            }
+            if (ablate & 2) {
+              a0[k] += v;
+              a1[k] ^= v;
+            } else {
+              mac(a0[k], v, kl[2 * j][256 * k + th]);
+              mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
+            }
           }
         }
       }
+      if constexpr (std::is_same<A, ArF64>::value) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
-        a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+        for (int k = 0; k < 8; k++) {
+          a0[k] = ar.canon(f0[k]);
+          a1[k] = ar.canon(f1[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+          a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+        }
+        (void)f0;
+        (void)f1;
       }
       if (t < lvl && t >= p_lo) {
         const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
@@ -2372,7 +2473,7 @@ void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t 
 // Montgomery-form copy of a key (x 2^64 mod q per limb), used by the fused
 // inner product.
 __global__ void to_mont_kernel(uint64_t *out, const uint64_t *in, unsigned logn, unsigned nmod, unsigned logn2,
-                               const ModConst *mc)
+                               int f64, const ModConst *mc)
 {
   const size_t n = (size_t)1 << logn;
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2382,7 +2483,8 @@ __global__ void to_mont_kernel(uint64_t *out, const uint64_t *in, unsigned logn,
   const size_t base = (size_t)blockIdx.y << logn;
   const ModConst m = mc[limb];
   const size_t dst = logn2 ? own_perm((unsigned)k) : k;
-  out[base + dst] = mul_mod(in[base + k], m.r64, m);
+  // moduli on the FP64 path multiply the plain key; the others use REDC
+  out[base + dst] = f64 && m.q < F64_QMAX ? in[base + k] : mul_mod(in[base + k], m.r64, m);
 }
 
 // Montgomery copy (x 2^64 mod q) of nlimbs_total limbs (limb slot = index %
@@ -2391,7 +2493,7 @@ void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
 {
   const unsigned logn2 = k_ks_fused_ok() ? ks_logn2() : 0;
   hipLaunchKernelGGL(to_mont_kernel, dim3((G.n + TPB - 1) / TPB, nlimbs_total), dim3(TPB), 0, G.stream, out, in,
-                     G.logn, G.nmod, logn2, G.dev.mc);
+                     G.logn, G.nmod, logn2, G.twd ? 1 : 0, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
