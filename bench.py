@@ -44,8 +44,10 @@ def parse():
     ap.add_argument("--dnum", type=int, default=2,
                     help="key-switch digits (2: fastest measured at L=8, see DESIGN.md; L: one limb per digit)")
     ap.add_argument("--nspecial", type=int, default=0, help="special primes K (default: enough for P > digit)")
-    ap.add_argument("--p-bits", type=int, default=60, help="special prime size in bits")
-    ap.add_argument("--q0-bits", type=int, default=60, help="first prime size in bits")
+    ap.add_argument("--p-bits", type=int, default=51, help="special prime size in bits")
+    ap.add_argument("--q0-bits", type=int, default=51, help="first prime size in bits")
+    ap.add_argument("--alt-bits", type=int, default=60,
+                    help="also time q0/special primes of this size (conventional CKKS sizes; 0: skip)")
     ap.add_argument("--no-cstr", action="store_true", help="skip the encrypted CSTR loop (config 4)")
     ap.add_argument("--cstr-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -137,7 +139,7 @@ def main():
         launches, tot_us, nbytes = stats[dom_name]
         achieved = nbytes / tot_us / 1e3  # GB/s
         workload = (f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, dnum={eng.info.dnum}, "
-                    f"batch={B} pairs per GPU")
+                    f"primes {args.q0_bits}/50/{args.p_bits} bits, batch={B} pairs per GPU")
         traffic, src = pmc_traffic(dom_name, workload)
         dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
@@ -160,7 +162,8 @@ def main():
             "data": "synthetic random-residue ciphertexts (splitmix64), real relinearization key",
             "config": {"workload": workload,
                        "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": K,
-                       "dnum": eng.info.dnum, "parallelism": f"batch-sharded x{world}"},
+                       "dnum": eng.info.dnum, "prime_bits": {"q0": args.q0_bits, "qi": 50, "p": args.p_bits},
+                       "parallelism": f"batch-sharded x{world}"},
             "event_s_rank0": ev_s,
             "op_roofline": {"alg_bytes_per_op": alg_bytes,
                             "achieved_GBs": alg_bytes * value / world / 1e9,
@@ -171,6 +174,9 @@ def main():
         }
     if rank == 0 and not args.no_ntt:
         result["ntt_roundtrip"] = ntt_roundtrip(eng, stream, logn, L, args.ntt_polys)
+    if rank == 0 and world == 1 and args.alt_bits and args.alt_bits != args.q0_bits:
+        eng.exit()
+        result["alt_primes"] = alt_rate(args, stream, L, logn, B, dnum)
     barrier()
     if rank == 0 and not args.no_cstr:
         eng.exit()
@@ -203,6 +209,40 @@ def pmc_traffic(kernel, workload):
             if (name == kernel or name.startswith(kernel.split("<")[0] + "<")) and "hbm_bytes" in e:
                 return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
     return None, None
+
+
+def alt_rate(args, stream, L, logn, B, dnum):
+    """The same op and batch with q0 and the special primes at args.alt_bits
+    (60: the conventional CKKS sizes).  Limbs of 51 bits and more take the
+    64-bit integer butterflies instead of the FP64 ones."""
+    from hectr_amd.gpqhe import Engine
+    bits = args.alt_bits
+    K = special_primes(L, dnum, q0_bits=bits, p_bits=bits)
+    eng = Engine.product()
+    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=bits, qi_bits=50, p_bits=bits,
+                    seed=1000)
+    eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
+    pk, sk, rlk = eng.pk(), eng.sk(), eng.evk()
+    eng.keypair(pk, sk)
+    eng.genrlk(rlk, sk)
+    import torch
+    n = 1 << logn
+    a = torch.empty(B * 2 * L * n, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    out = torch.empty(B * 2 * (L - 1) * n, dtype=torch.int64, device="cuda")
+    from hectr_amd import dist as hdist
+    hdist.fill_pairs(eng.lib, a.data_ptr(), b.data_ptr(), 0, B, L, n)
+    for _ in range(max(1, args.warmup)):
+        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
+    eng.sync()
+    dt = time.perf_counter() - t0
+    eng.exit()
+    return {"q0_bits": bits, "qi_bits": 50, "p_bits": bits, "nspecial": K, "value": B * args.steps / dt,
+            "unit": "ct-mult/s", "steps": args.steps}
 
 
 def ntt_roundtrip(eng, stream, logn, L, polys, reps=3):
