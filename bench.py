@@ -205,9 +205,14 @@ def pmc_traffic(kernel, workload):
             continue
         if d.get("meta", {}).get("bench_workload") != workload:
             continue
+        base, _, tag = kernel.partition("<")
+        flag = {"fwd>": "false>", "inv>": "true>"}.get(tag)
         for name, e in d.get("kernels", {}).items():
-            if (name == kernel or name.startswith(kernel.split("<")[0] + "<")) and "hbm_bytes" in e:
-                return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
+            if name.split("<")[0] != base or "hbm_bytes" not in e:
+                continue
+            if flag and not name.endswith(flag):
+                continue
+            return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
     return None, None
 
 

@@ -41,13 +41,17 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
   KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
-  KC_DN_ROWS, KC_COUNT
+  KC_DN_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
+  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_COUNT
 };
+// kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
+// for the INV flag), so bench.py can match its statistics to a PMC profile
 static const char *kc_names[KC_COUNT] = {
-  "ntt_whole_kernel<false>", "ntt_whole_kernel<true>", "ntt_cols_kernel<false>", "ntt_rows_kernel<false>",
-  "ntt_rows_kernel<true>", "ntt_cols_kernel<true>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
+  "ntt_whole_kernel<fwd>", "ntt_whole_kernel<inv>", "ntt_cols_kernel<fwd>", "ntt_rows_kernel<fwd>",
+  "ntt_rows_kernel<inv>", "ntt_cols_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
-  "dn_rows_kernel"};
+  "dn_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
+  "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -1023,11 +1027,11 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   static const bool rows8 = !getenv("GPQHE_NTT2ROWS");
   if (!inverse) {
     {
-      ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
+      ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
       hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
                          G.dev.mc, (const uint64_t *)nullptr);
     }
-    ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
+    ProfScope ps(rows8 ? KC_NTT3_ROWS_FWD : KC_NTT2_ROWS_FWD, pass_bytes);
     if (rows8)
       hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
                          G.dev.mc);
@@ -1036,7 +1040,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
                          G.dev.mc);
   } else {
     {
-      ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
+      ProfScope ps(rows8 ? KC_NTT3_ROWS_INV : KC_NTT2_ROWS_INV, pass_bytes);
       if (rows8)
         hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn,
                            tw, G.dev.mc);
@@ -1044,7 +1048,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
         hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
                            G.dev.mc);
     }
-    ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
+    ProfScope ps(KC_NTT2_COLS_INV, pass_bytes);
     hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
                        G.dev.mc, post);
   }
@@ -2371,7 +2375,7 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   {
     // reads the digit's alpha limbs once per target set (registers), writes
     // the converted + column-transformed limbs
-    ProfScope ps(KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
+    ProfScope ps(rowform || G.alpha <= 4 ? KC_KS_COLS4 : KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
     const unsigned ngroups = tiles * count * ndig;
     if (rowform) {
       constexpr unsigned NT = 8;  // all targets of a digit tile: its INTT columns run once
@@ -2393,9 +2397,11 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     }
   }
   // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key once, writes acc
-  ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
+  const bool rows2 = ndig == 2 && !getenv("GPQHE_KSROWS_STREAM");
+  ProfScope ps(rows2 ? KC_KS_ROWS2 : KC_KS_ROWS,
+               8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
                                                        2 * nm) + 2.0 * ndig * nm));
-  if (ndig == 2 && !getenv("GPQHE_KSROWS_STREAM")) {
+  if (rows2) {
     // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
     const unsigned groups = nm * (n / 2048);
     static const unsigned want = getenv("GPQHE_KSR_MEMBERS") ? atoi(getenv("GPQHE_KSR_MEMBERS")) : 0;

@@ -9,7 +9,7 @@ mkdir -p $OUT
 if [ -z "$NO_FULL" ]; then
   timeout -k 10 600 python bench.py > $OUT/bench_full.log 2>&1 || exit 1
 fi
-B="python bench.py --steps 3 --warmup 1 --no-cpu --no-cstr"
+B="python bench.py --steps 3 --warmup 1 --no-cpu --no-cstr --no-ntt --alt-bits 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B > $OUT/kt.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $B > $OUT/fetch.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- $B > $OUT/write.log 2>&1 || exit 1
