@@ -591,11 +591,10 @@ struct ArF64 {
 
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
 
-// Debug ablation mask for timing studies (GPQHE_ABLATE; results are wrong
-// when set): ks_rows2: 1 skip row NTT, 2 skip key MAC, 4 skip acc stores, 8
-// skip the inverse row pass; dn_cols: 16 skip the loader INTT, 32 skip the
-// conversion, 64 skip the target NTT; ks_cols4: 128 skip the conversion, 256
-// skip the target NTT.
+// Debug ablation mask for timing studies of ks_rows2 (GPQHE_ABLATE; results
+// are wrong when set): 1 skip row NTT, 2 skip key MAC, 4 skip acc stores, 8
+// skip the inverse row pass.  (dn_cols / ks_cols4 were studied the same way;
+// DESIGN.md 5 records the split.)
 static const int g_ablate = getenv("GPQHE_ABLATE") ? atoi(getenv("GPQHE_ABLATE")) : 0;
 
 // Run f with the arithmetic policy of modulus index m (q = its prime).
@@ -1851,7 +1850,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
                                                            size_t t1_stride, unsigned logn, unsigned lvl,
                                                            unsigned L, unsigned nm, unsigned ndig, unsigned members,
                                                            unsigned ngroups, UpTable tab, Tw2 tw,
-                                                           const ModConst *mcs, int ablate)
+                                                           const ModConst *mcs)
 {
   constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
   __shared__ __attribute__((aligned(16))) uint64_t lds[2][T * CP];
@@ -1952,18 +1951,13 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         V r[EA];
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          if (ablate & 128) {
-            r[k] = A::load(y[it][0][k] ^ y[it][3][k]);
-            continue;
-          }
           unsigned __int128 acc = 0;
 #pragma unroll
           for (int i = 0; i < 4; i++)
             acc += (unsigned __int128)y[it][i][k] * cc[i];
           r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
         }
-        if (!(ablate & 256))
-          ar.template fwd<LEA>(r, T, LOGT - 1);
+        ar.template fwd<LEA>(r, T, LOGT - 1);
 #pragma unroll
         for (int k = 0; k < EA; k++)
           buf[(l + 16 * k) * CP + c] = A::bits(r[k]);
@@ -1974,8 +1968,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
 #pragma unroll
       for (int k = 0; k < 16; k++)
         r[k] = A::unbits(buf[(16 * g + k) * CP + c]);
-      if (!(ablate & 256))
-        ar.template fwd<4>(r, T + 16 * g, 3);
+      ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
         out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
@@ -2392,14 +2385,14 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
       const unsigned members = (nm - na_min + NT - 1) / NT;
       hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
                          G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
-                         tw, G.dev.mc, g_ablate);
+                         tw, G.dev.mc);
     } else if (G.alpha <= 4) {
       constexpr unsigned NT = 4;
       const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
       hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
                          G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
-                         tw, G.dev.mc, g_ablate);
+                         tw, G.dev.mc);
     } else {
       hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
@@ -2702,7 +2695,7 @@ template <int LOGT, int NT, bool X5>
 __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, uint64_t *conv,
                                                           unsigned logn, unsigned lvl, unsigned L, unsigned members,
                                                           unsigned ngroups, DownTable tab, Tw2 tw,
-                                                          const ModConst *mcs, int ablate)
+                                                          const ModConst *mcs)
 {
   constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
   __shared__ __attribute__((aligned(16))) uint64_t lds[T * CP];
@@ -2740,8 +2733,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 #pragma unroll
         for (int k = 0; k < 16; k++)
           r[k] = A::load(src[(size_t)(16 * g + k) * n2 + c]);
-        if (!(ablate & 16))
-          ar.template inv<4>(r, T + 16 * g, 0);
+        ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
         for (int k = 0; k < 16; k++)
           lds[(16 * g + k) * CP + c] = A::bits(r[k]);
@@ -2754,11 +2746,10 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 #pragma unroll
         for (int k = 0; k < EA; k++)
           r[k] = A::unbits(lds[(l + 16 * k) * CP + c]);
-        if (!(ablate & 16))
-          ar.template inv<LEA>(r, T, 4);
+        ar.template inv<LEA>(r, T, 4);
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          const uint64_t v = (ablate & 16) ? A::bits(r[k]) : ar.mulc(r[k], w, wp);
+          const uint64_t v = ar.mulc(r[k], w, wp);
           if (d < 4)
             y[it][d < 4 ? d : 0][k] = v;
           else if constexpr (X5)
@@ -2799,10 +2790,6 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
         V r[EA];
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          if (ablate & 32) {
-            r[k] = A::load(y[it][0][k] ^ y[it][3][k]);
-            continue;
-          }
           unsigned __int128 acc = 0;
 #pragma unroll
           for (int d = 0; d < 4; d++)
@@ -2811,8 +2798,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
             acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
           r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
         }
-        if (!(ablate & 64))
-          ar.template fwd<LEA>(r, T, LOGT - 1);
+        ar.template fwd<LEA>(r, T, LOGT - 1);
 #pragma unroll
         for (int k = 0; k < EA; k++)
           lds[(l + 16 * k) * CP + c] = A::bits(r[k]);
@@ -2823,8 +2809,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 #pragma unroll
       for (int k = 0; k < 16; k++)
         r[k] = A::unbits(lds[(16 * g + k) * CP + c]);
-      if (!(ablate & 64))
-        ar.template fwd<4>(r, T + 16 * g, 3);
+      ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
         out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
@@ -2904,12 +2889,10 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
     const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
     if (tab.nd <= 4)
       hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc,
-                         g_ablate);
+                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     else
       hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc,
-                         g_ablate);
+                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
   }
   // reads conv, X and d01 keep limbs, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
