@@ -1891,36 +1891,38 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         return;
       }
       const unsigned mi_ = lo + i;
-      const uint64_t qi = mcs[mi_].q;
-      const uint64_t *itw2 = tw.inv + ((size_t)mi_ << (logn + 1));
       const uint64_t w = tab.ysc1[2 * mi_], wp = tab.ysc1[2 * mi_ + 1];
       const uint64_t *src = yb + ((size_t)i << logn);
       if (i)
         __syncthreads();
-      {
-        const int c = th % C, g = th / C;
-        uint64_t r[16];
+      with_arith(mcs[mi_].q, mi_, logn, tw, [&](const auto &ar) {
+        using A = std::decay_t<decltype(ar)>;
+        using V = typename A::V;
+        {
+          const int c = th % C, g = th / C;
+          V r[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-          r[k] = src[(size_t)(16 * g + k) * n2 + c];
-        inv_stages<4>(r, itw2, T + 16 * g, 0, qi);
+          for (int k = 0; k < 16; k++)
+            r[k] = A::load(src[(size_t)(16 * g + k) * n2 + c]);
+          ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-          lds[0][(16 * g + k) * CP + c] = r[k];
-      }
-      __syncthreads();
+          for (int k = 0; k < 16; k++)
+            lds[0][(16 * g + k) * CP + c] = A::bits(r[k]);
+        }
+        __syncthreads();
 #pragma unroll
-      for (int it = 0; it < IT; it++) {
-        const int item = th + 256 * it, c = item % C, l = item / C;
-        uint64_t r[EA];
+        for (int it = 0; it < IT; it++) {
+          const int item = th + 256 * it, c = item % C, l = item / C;
+          V r[EA];
 #pragma unroll
-        for (int k = 0; k < EA; k++)
-          r[k] = lds[0][(l + 16 * k) * CP + c];
-        inv_stages<LEA>(r, itw2, T, 4, qi);
+          for (int k = 0; k < EA; k++)
+            r[k] = A::unbits(lds[0][(l + 16 * k) * CP + c]);
+          ar.template inv<LEA>(r, T, 4);
 #pragma unroll
-        for (int k = 0; k < EA; k++)
-          y[it][i][k] = mul_shoup(r[k], w, wp, qi);
-      }
+          for (int k = 0; k < EA; k++)
+            y[it][i][k] = ar.mulc(r[k], w, wp);
+        }
+      });
     };
     load_limb(std::integral_constant<int, 0>{});
     load_limb(std::integral_constant<int, 1>{});
