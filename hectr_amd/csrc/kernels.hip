@@ -1030,7 +1030,8 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const unsigned blocks = s.count * (n / 4096);
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const double pass_bytes = 16.0 * n * s.count;
-  static const bool rows8 = !getenv("GPQHE_NTT2ROWS");
+  static const bool rows8_env = !getenv("GPQHE_NTT2ROWS");
+  const bool rows8 = rows8_env || LOGN2 > 8;  // the 16-element row kernels need 4096 / N2 >= 16 rows
   if (!inverse) {
     {
       ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
@@ -1041,7 +1042,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
     if (rows8)
       hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
                          G.dev.mc);
-    else
+    else if constexpr (LOGN2 <= 8)
       hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
                          G.dev.mc);
   } else {
@@ -1050,7 +1051,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
       if (rows8)
         hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn,
                            tw, G.dev.mc);
-      else
+      else if constexpr (LOGN2 <= 8)
         hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
                            G.dev.mc);
     }
@@ -1064,7 +1065,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
 // v2 path available for this ring degree?
 static bool ntt2_ok()
 {
-  return G.logn >= 13 && G.logn <= 16 && !getenv("GPQHE_NTT_V1");
+  return G.logn >= 13 && G.logn <= 17 && !getenv("GPQHE_NTT_V1");
 }
 
 // Out-of-place NTT (in and out have the same geometry; out may equal in);
@@ -1078,6 +1079,7 @@ void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_
   case 14: ntt2_launch<7, 7>(in, out, inverse, post); return;
   case 15: ntt2_launch<7, 8>(in, out, inverse, post); return;
   case 16: ntt2_launch<8, 8>(in, out, inverse, post); return;
+  case 17: ntt2_launch<8, 9>(in, out, inverse, post); return;
   default: gpqhe_die("k_ntt_ex: ring degree 2^%u not supported", G.logn);
   }
 }
@@ -1482,7 +1484,7 @@ struct UpTable {
 // Row length n2 of the fused kernels' 4-step split (n = n1 x n2).
 static unsigned ks_logn2()
 {
-  return G.logn >= 15 ? 8 : 7;
+  return G.logn >= 17 ? 9 : G.logn >= 15 ? 8 : 7;
 }
 
 static std::map<unsigned, UpTable> g_up;
@@ -2451,7 +2453,7 @@ void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t 
   // Row form removes the d2 INTT but lengthens the (latency-bound) tensor,
   // ks_cols and ks_rows kernels by more than it saves (20.1k vs 20.7k op/s at
   // N=2^16, L=8); opt-in until those kernels are pipelined.
-  const bool rowform = G.alpha <= 4 && getenv("GPQHE_KS_ROWFORM");
+  const bool rowform = G.alpha <= 4 && G.logn <= 16 && getenv("GPQHE_KS_ROWFORM");
   if (rowform) {
     // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
     if (ks_logn2() == 8)
@@ -2476,7 +2478,8 @@ void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t 
   case 14: ks_fused_launch<7, 7>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
   case 15: ks_fused_launch<7, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
   case 16: ks_fused_launch<8, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^16");
+  case 17: ks_fused_launch<8, 9>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
   }
 }
 
@@ -2917,7 +2920,8 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
   case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
   case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
   case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
-  default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^16");
+  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
   if (!conv_ws)
     pool_free(conv);

@@ -13,6 +13,8 @@ Parameter sets:
   c5    : config 5 sizes, n=2^17, L=12, K=4, dnum=3 (the multi-GPU config)
   bench51: the bench shape with every prime below 2^51, so every NTT and the
           key inner product run on the FP64 path
+  c17   : n=2^17, L=8, K=4, dnum=2, primes < 2^51 (the 2^17 fused path with the
+          key-stationary two-digit inner product)
 Integer results must match exactly; decoded values are compared with the
 closed-loop tolerance of the CSTR test (1e-6 relative, reference achieves
 1e-11).
@@ -33,6 +35,7 @@ PARAMS = {
     "c5": ("params", dict(logn=17, nlimbs=12, nspecial=4, dnum=3, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
     "bench51": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50,
                                p_bits=51)),
+    "c17": ("params", dict(logn=17, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50, p_bits=51)),
 }
 
 
@@ -154,7 +157,8 @@ def test_ntt_batch_bitexact(oracle, product, name):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51", "c5"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51", "c5",
+                                  "c17"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
     latter also through the opt-in row-form key switch and through the
