@@ -935,6 +935,14 @@ void gemv_cache_clear()
   g_gemv_cache_bytes = 0;
 }
 
+// Would encoding one more diagonal at this level overflow the cache (and so
+// clear it)?  he_gemv flushes its pending launch before that happens.
+static bool diag_cache_full(unsigned lvl)
+{
+  const size_t bytes = ((size_t)(lvl + G.K) << G.logn) * 8;
+  return g_gemv_cache_bytes + bytes > ((size_t)1 << 31);
+}
+
 static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
 {
   std::string key((const char *)diag, (size_t)s * 16);
@@ -965,8 +973,20 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   const double *Md = (const double *)M;
   Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
   hoist_modup(D.p, x, lvl);
-  HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   std::vector<double> diag(2 * (size_t)s);
+  // all non-zero diagonals in as few launches as possible (32 per launch)
+  GemvDiags dg{};
+  bool started = false;
+  auto flush = [&]() {
+    if (!dg.count)
+      return;
+    k_gemv_inner(acc.p, D.p, limb(x, 0, 0), limb(x, 1, 0), lvl, dg, started);
+    started = true;
+    dg.count = 0;
+  };
+  const bool batched = !getenv("GPQHE_GEMV_PER_DIAG");
+  if (!batched)
+    HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   for (unsigned d = 0; d < s; d++) {
     bool nz = false;
     for (unsigned i = 0; i < s; i++) {
@@ -977,14 +997,28 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     }
     if (!nz)
       continue;
+    if (batched && diag_cache_full(lvl))
+      flush();  // the cache may be cleared below: launch what refers to it first
     const uint64_t *pt = diag_pt(diag.data(), s, lvl);
-    if (d == 0) {
-      k_ks_inner(acc.p, D.p, 1, 0, 0, nullptr, lvl, 1, limb(x, 0, 0), limb(x, 1, 0), 0, pt, true);
+    const uint64_t g = d == 0 ? 1 : galois_of_rot(d);
+    const he_evk_t *k = d == 0 ? nullptr : find_rot_key(rk, d, g);
+    if (batched) {
+      dg.evk[dg.count] = k ? k->data : nullptr;
+      dg.pt[dg.count] = pt;
+      dg.g[dg.count] = g;
+      if (++dg.count == GemvDiags::MAX)
+        flush();
       continue;
     }
-    const uint64_t g = galois_of_rot(d);
-    const he_evk_t *k = find_rot_key(rk, d, g);
-    k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(x, 0, 0), nullptr, 0, pt, true);
+    if (d == 0)
+      k_ks_inner(acc.p, D.p, 1, 0, 0, nullptr, lvl, 1, limb(x, 0, 0), limb(x, 1, 0), 0, pt, true);
+    else
+      k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(x, 0, 0), nullptr, 0, pt, true);
+  }
+  if (batched) {
+    flush();
+    if (!started)  // all-zero matrix
+      HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   }
   const double scale = x->scale;
   k_moddown(y->data, pstride(y), acc.p, nm * n, 2, lvl, 1);

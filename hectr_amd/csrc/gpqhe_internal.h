@@ -257,6 +257,16 @@ void k_automorph(uint64_t *out, const uint64_t *in, unsigned nlimbs, uint64_t g)
 void k_square(uint64_t *out, const uint64_t *in, unsigned nlimbs);
 void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl);
 // acc [count][2][lvl+K][n] (stride acc_stride): acc0 then acc1
+// he_gemv diagonals of one launch (passed by value as kernel arguments)
+struct GemvDiags {
+  static constexpr unsigned MAX = 32;
+  const uint64_t *evk[MAX];  // key of the rotation, nullptr for the identity
+  const uint64_t *pt[MAX];   // encoded diagonal (over basis_qp(lvl))
+  uint64_t g[MAX];           // Galois element (1: identity)
+  unsigned count;
+};
+void k_gemv_inner(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1, unsigned lvl,
+                  const GemvDiags &dg, bool accumulate);
 void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_stride, size_t acc_stride,
                 const uint64_t *evk, unsigned lvl, uint64_t g, const uint64_t *c0, const uint64_t *c1,
                 size_t c_stride, const uint64_t *pt, bool accumulate);

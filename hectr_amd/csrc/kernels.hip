@@ -1663,6 +1663,65 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
   (void)c_pstride;
 }
 
+// he_gemv's diagonal sum in one launch: for each non-zero diagonal e,
+//   acc0 += pt_e * (sum_j D_j[perm_e k] evk_e,b[j] + [P] x0[perm_e k])
+//   acc1 += pt_e * (sum_j D_j[perm_e k] evk_e,a[j])          (rotations)
+//   acc0 += pt_e * [P] x0[k], acc1 += pt_e * [P] x1[k]        (identity)
+// with the hoisted ModUp D of x; replaces one ks_inner launch per diagonal.
+// grid: (n / TPB, nm).
+__global__ void gemv_inner_kernel(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1,
+                                  unsigned logn, unsigned lvl, unsigned L, unsigned nm, unsigned nmod,
+                                  unsigned ndig, GemvDiags dg, int accumulate, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n)
+    return;
+  const unsigned t = blockIdx.y;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mm = mc[m];
+  const size_t tl = (size_t)t << logn;
+  uint64_t a0 = 0, a1 = 0;
+  for (unsigned e = 0; e < dg.count; e++) {
+    const uint64_t g = dg.g[e];
+    const size_t src = g == 1 ? k : auto_index((unsigned)k, g, logn);
+    uint64_t s0 = 0, s1 = 0;
+    const uint64_t *evk = dg.evk[e];
+    if (evk) {
+      for (unsigned j = 0; j < ndig; j++) {
+        const uint64_t dv = D[(((size_t)j * nm) << logn) + tl + src];
+        s0 = add_mod(s0, mul_mod(dv, evk[(((size_t)(2 * j) * nmod + m) << logn) + k], mm), mm.q);
+        s1 = add_mod(s1, mul_mod(dv, evk[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mm), mm.q);
+      }
+    }
+    if (t < lvl) {
+      s0 = add_mod(s0, mul_shoup(x0[tl + src], mm.pmod, mm.pmodp, mm.q), mm.q);
+      if (!evk)
+        s1 = add_mod(s1, mul_shoup(x1[tl + src], mm.pmod, mm.pmodp, mm.q), mm.q);
+    }
+    const uint64_t w = dg.pt[e][tl + k];
+    a0 = add_mod(a0, mul_mod(w, s0, mm), mm.q);
+    a1 = add_mod(a1, mul_mod(w, s1, mm), mm.q);
+  }
+  uint64_t *o0 = acc + tl + k, *o1 = o0 + ((size_t)nm << logn);
+  if (accumulate) {
+    a0 = add_mod(a0, *o0, mm.q);
+    a1 = add_mod(a1, *o1, mm.q);
+  }
+  *o0 = a0;
+  *o1 = a1;
+}
+
+void k_gemv_inner(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1, unsigned lvl,
+                  const GemvDiags &dg, bool accumulate)
+{
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  ProfScope ps(KC_KS_INNER, 8.0 * G.n * (double)dg.count * (ndig * nm + 2 * nm + 2 * lvl));
+  hipLaunchKernelGGL(gemv_inner_kernel, dim3((G.n + TPB - 1) / TPB, nm), dim3(TPB), 0, G.stream, acc, D, x0, x1,
+                     G.logn, lvl, G.L, nm, G.nmod, ndig, dg, accumulate ? 1 : 0, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
 // acc layout per ciphertext p: acc0 at acc + p*acc_stride, acc1 right after
 // it (nm limbs later).
 void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_stride, size_t acc_stride,
