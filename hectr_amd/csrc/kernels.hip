@@ -42,7 +42,7 @@ enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
   KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
   KC_DN_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
-  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_COUNT
+  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
@@ -51,7 +51,8 @@ static const char *kc_names[KC_COUNT] = {
   "ntt_rows_kernel<inv>", "ntt_cols_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
   "dn_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
-  "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel"};
+  "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel",
+  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>"};
 
 struct ProfEntry {
   int cls;
@@ -1084,6 +1085,115 @@ void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_
   }
 }
 
+// Whole-limb NTT for n = 2^10 .. 2^12 (HECTR's own ring): one block of n/8
+// threads per limb, radix-8 register rounds (3 stages each, the last round
+// takes the remaining logn mod 3 stages on 8 / 2^r groups per thread), lazy
+// butterflies on the limb's arithmetic policy.  Round r covers global stages
+// [3r, 3r + 3): thread t's group starts at pos0 = (t / D8) 8 D8 + t % D8 with
+// D8 = n >> (3r + 3) the group's smallest distance, twiddle base n + pos0.
+template <int LOGN, bool INV>
+__global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs)
+{
+  constexpr int n = 1 << LOGN, NT = n / 8, FULL = LOGN / 3, REM = LOGN % 3;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned v = blockIdx.x;
+  uint64_t *x = s.limb(v, LOGN);
+  const unsigned m = s.mod(v);
+  const ModConst mc = mcs[m];
+  const int th = threadIdx.x;
+  with_arith(mc.q, m, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    using V = typename A::V;
+    // elements of a radix-8 group of round r (distances n>>(3r+1) .. n>>(3r+3))
+    auto group = [&](int r, int &pos0, int &d8) {
+      d8 = n >> (3 * r + 3);
+      pos0 = (th / d8) * 8 * d8 + th % d8;
+    };
+    V a[8];
+    if constexpr (!INV) {
+#pragma unroll
+      for (int r = 0; r < FULL; r++) {
+        int pos0, d8;
+        group(r, pos0, d8);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          a[k] = r ? A::unbits(lds[pos0 + k * d8]) : A::load(x[pos0 + k * d8]);
+        ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
+        if (r + 1 < FULL || REM) {
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            lds[pos0 + k * d8] = A::bits(a[k]);
+          __syncthreads();
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            x[pos0 + k * d8] = ar.canon(a[k]);
+        }
+      }
+      if constexpr (REM > 0) {
+        // last REM stages (distances 2^(REM-1) .. 1): thread t owns 8
+        // consecutive elements = 8 / 2^REM groups
+        constexpr int EG = 1 << REM;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          a[k] = A::unbits(lds[8 * th + k]);
+#pragma unroll
+        for (int j = 0; j < 8 / EG; j++) {
+          V g[EG];
+#pragma unroll
+          for (int e = 0; e < EG; e++)
+            g[e] = a[j * EG + e];
+          ar.template fwd<REM>(g, (uint64_t)n + 8 * th + EG * j, REM - 1);
+#pragma unroll
+          for (int e = 0; e < EG; e++)
+            x[8 * th + j * EG + e] = ar.canon(g[e]);
+        }
+      }
+    } else {
+      if constexpr (REM > 0) {
+        constexpr int EG = 1 << REM;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          a[k] = A::load(x[8 * th + k]);
+#pragma unroll
+        for (int j = 0; j < 8 / EG; j++) {
+          V g[EG];
+#pragma unroll
+          for (int e = 0; e < EG; e++)
+            g[e] = a[j * EG + e];
+          ar.template inv<REM>(g, (uint64_t)n + 8 * th + EG * j, 0);
+#pragma unroll
+          for (int e = 0; e < EG; e++)
+            lds[8 * th + j * EG + e] = A::bits(g[e]);
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int rr = 0; rr < FULL; rr++) {
+        const int r = FULL - 1 - rr;  // smallest distances first
+        int pos0, d8;
+        group(r, pos0, d8);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          a[k] = (rr || REM) ? A::unbits(lds[pos0 + k * d8]) : A::load(x[pos0 + k * d8]);
+        ar.template inv<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 3);
+        if (rr + 1 < FULL) {
+          __syncthreads();  // every group of this round has read its inputs
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            lds[pos0 + k * d8] = A::bits(a[k]);
+          __syncthreads();
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            x[pos0 + k * d8] = ar.mulc(a[k], mc.ninv, mc.ninvp);
+        }
+      }
+    }
+  });
+  (void)NT;
+}
+
 void k_ntt(const LimbSet &s, bool inverse)
 {
   if (!s.count)
@@ -1091,6 +1201,21 @@ void k_ntt(const LimbSet &s, bool inverse)
   const unsigned logn = G.logn, n = G.n;
   if (s.count > 65535)
     gpqhe_die("k_ntt: %u limbs in one launch", s.count);
+  if (logn >= 10 && logn <= 12 && !getenv("GPQHE_NTT_WHOLE_V1")) {
+    ProfScope ps(inverse ? KC_NTT_SMALL_INV : KC_NTT_SMALL_FWD, 16.0 * n * s.count);
+    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+    auto go = [&](auto kern, unsigned threads) {
+      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc);
+    };
+    if (logn == 12)
+      inverse ? go(ntt_small_kernel<12, true>, 512) : go(ntt_small_kernel<12, false>, 512);
+    else if (logn == 11)
+      inverse ? go(ntt_small_kernel<11, true>, 256) : go(ntt_small_kernel<11, false>, 256);
+    else
+      inverse ? go(ntt_small_kernel<10, true>, 128) : go(ntt_small_kernel<10, false>, 128);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (logn <= 12) {
     ProfScope ps(inverse ? KC_NTT_WHOLE_INV : KC_NTT_WHOLE_FWD, 16.0 * n * s.count);
     if (inverse)
