@@ -667,11 +667,17 @@ extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
   unsigned mods[GPQHE_MAXMOD];
   for (unsigned i = 0; i < lvl; i++)
     mods[i] = i;
-  Ws v(w), e0(w), e1(w);
-  sample_small_ntt(v.p, mods, lvl, 0);
-  sample_small_ntt(e0.p, mods, lvl, 1);
-  sample_small_ntt(e1.p, mods, lvl, 1);
-  k_enc_combine(limb(ct, 0, 0), limb(ct, 1, 0), v.p, e0.p, e1.p, limb(pk, 0, 0), limb(pk, 1, 0), pt->data, lvl);
+  // v (ternary), e0, e1 (CBD) on consecutive streams, sampled and NTT'd in
+  // one launch each (the values of three sample_small_ntt calls in order)
+  Ws vee(3 * w);
+  LimbSet s = limbset(vee.p, mods, lvl, 3, w);
+  const uint64_t stream = next_stream();
+  next_stream();
+  next_stream();
+  k_sample_enc(s, stream, 3);
+  k_ntt(s, false);
+  k_enc_combine(limb(ct, 0, 0), limb(ct, 1, 0), vee.p, vee.p + w, vee.p + 2 * w, limb(pk, 0, 0), limb(pk, 1, 0),
+                pt->data, lvl);
   ct->nlimbs = lvl;
   ct->scale = pt->scale;
   ct->flags = 0;

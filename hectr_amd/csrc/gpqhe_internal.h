@@ -244,6 +244,7 @@ void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t pstride);
 void k_tensor(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b, unsigned lvl,
               size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride);
 void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned lvl);
+void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);
 void k_lift_i64(const LimbSet &dst, const int64_t *coef);

@@ -1370,6 +1370,38 @@ __global__ void sample_small_kernel(LimbSet dst, unsigned logn, ChachaKey key, u
   }
 }
 
+// Encryption noise in one launch: polynomial y of `npoly` (rows of dst.per
+// limbs) draws from ChaCha stream `stream + y`; y = 0 is ternary (v), the
+// others CBD (e0, e1) -- the same streams and values as npoly separate
+// k_sample_small calls in that order.
+__global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, const ModConst *mc)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (1u << logn))
+    return;
+  const unsigned y = blockIdx.y;
+  uint32_t b[16];
+  chacha20_block(b, key, stream + y, k);
+  int v;
+  if (y) {
+    v = __popc(b[0] & 0x1FFFFFu) - __popc(b[1] & 0x1FFFFFu);
+  } else {
+    const uint32_t r = b[0] & 3u;
+    v = r < 2 ? 0 : (r == 2 ? 1 : -1);
+  }
+  for (unsigned l = y * dst.per; l < (y + 1) * dst.per; l++) {
+    const uint64_t q = mc[dst.mod(l)].q;
+    dst.limb(l, logn)[k] = v >= 0 ? (uint64_t)v : q - (uint64_t)(-v);
+  }
+}
+
+void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly)
+{
+  hipLaunchKernelGGL(sample_enc_kernel, dim3((G.n + TPB - 1) / TPB, npoly), dim3(TPB), 0, G.stream, dst, G.logn,
+                     G.key, stream, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd)
 {
   hipLaunchKernelGGL(sample_small_kernel, grid1(G.n), dim3(TPB), 0, G.stream, dst, G.logn, G.key, stream, cbd,
