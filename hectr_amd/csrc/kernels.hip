@@ -42,7 +42,7 @@ enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
   KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
   KC_DN_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
-  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_COUNT
+  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
@@ -52,7 +52,7 @@ static const char *kc_names[KC_COUNT] = {
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
   "dn_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel",
-  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>"};
+  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>", "gemv_inner_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -1825,21 +1825,23 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
 //   acc1 += pt_e * (sum_j D_j[perm_e k] evk_e,a[j])          (rotations)
 //   acc0 += pt_e * [P] x0[k], acc1 += pt_e * [P] x1[k]        (identity)
 // with the hoisted ModUp D of x; replaces one ks_inner launch per diagonal.
-// grid: (n / TPB, nm).
-__global__ void gemv_inner_kernel(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1,
-                                  unsigned logn, unsigned lvl, unsigned L, unsigned nm, unsigned nmod,
-                                  unsigned ndig, GemvDiags dg, int accumulate, const ModConst *mc)
+// A block covers 32 coefficients of one basis slot with 8 diagonal lanes
+// (thread (c, g) sums diagonals g, g + 8, ...); the 8 partial sums meet in
+// LDS.  grid: (n / 32, nm), 256 threads.
+__global__ void __launch_bounds__(256) gemv_inner_kernel(uint64_t *acc, const uint64_t *D, const uint64_t *x0,
+                                                          const uint64_t *x1, unsigned logn, unsigned lvl,
+                                                          unsigned L, unsigned nm, unsigned nmod, unsigned ndig,
+                                                          GemvDiags dg, int accumulate, const ModConst *mc)
 {
-  const size_t n = (size_t)1 << logn;
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n)
-    return;
+  __shared__ uint64_t part[2][8][32];
+  const unsigned c = threadIdx.x % 32, gl = threadIdx.x / 32;
+  const size_t k = (size_t)blockIdx.x * 32 + c;
   const unsigned t = blockIdx.y;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mm = mc[m];
   const size_t tl = (size_t)t << logn;
   uint64_t a0 = 0, a1 = 0;
-  for (unsigned e = 0; e < dg.count; e++) {
+  for (unsigned e = gl; e < dg.count; e += 8) {
     const uint64_t g = dg.g[e];
     const size_t src = g == 1 ? k : auto_index((unsigned)k, g, logn);
     uint64_t s0 = 0, s1 = 0;
@@ -1860,22 +1862,26 @@ __global__ void gemv_inner_kernel(uint64_t *acc, const uint64_t *D, const uint64
     a0 = add_mod(a0, mul_mod(w, s0, mm), mm.q);
     a1 = add_mod(a1, mul_mod(w, s1, mm), mm.q);
   }
-  uint64_t *o0 = acc + tl + k, *o1 = o0 + ((size_t)nm << logn);
-  if (accumulate) {
-    a0 = add_mod(a0, *o0, mm.q);
-    a1 = add_mod(a1, *o1, mm.q);
+  part[0][gl][c] = a0;
+  part[1][gl][c] = a1;
+  __syncthreads();
+  if (gl < 2) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      r = add_mod(r, part[gl][i][c], mm.q);
+    uint64_t *o = acc + ((size_t)gl * nm << logn) + tl + k;
+    *o = accumulate ? add_mod(r, *o, mm.q) : r;
   }
-  *o0 = a0;
-  *o1 = a1;
 }
 
 void k_gemv_inner(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1, unsigned lvl,
                   const GemvDiags &dg, bool accumulate)
 {
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
-  ProfScope ps(KC_KS_INNER, 8.0 * G.n * (double)dg.count * (ndig * nm + 2 * nm + 2 * lvl));
-  hipLaunchKernelGGL(gemv_inner_kernel, dim3((G.n + TPB - 1) / TPB, nm), dim3(TPB), 0, G.stream, acc, D, x0, x1,
-                     G.logn, lvl, G.L, nm, G.nmod, ndig, dg, accumulate ? 1 : 0, G.dev.mc);
+  ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * (double)dg.count * (ndig * nm + 2 * nm + 2 * lvl));
+  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 32, nm), dim3(256), 0, G.stream, acc, D, x0, x1, G.logn, lvl,
+                     G.L, nm, G.nmod, ndig, dg, accumulate ? 1 : 0, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
