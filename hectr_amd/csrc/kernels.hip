@@ -2412,7 +2412,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
   const uint64_t q = mc.q, q2 = 2 * q;
   const unsigned row0 = tile * T::R;
   const size_t toff = (size_t)row0 << LOGN2;
-  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
   // digit j's input for ciphertext p: own digit -> the NTT-form d2 limb
   // (natural layout, transposed through LDS), else T1[j][t] (row pass input)
   const bool own0 = t < lvl && t / alpha == 0, own1 = t < lvl && t / alpha == 1;
@@ -2425,9 +2425,14 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
   auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
     const uint64_t *s_ = src(j, p);
     if (j ? nat1 : nat0) {
+      // round C ownership is natural order: thread th holds words 8 th .. 8 th + 7
+      const ulonglong2 *v2 = (const ulonglong2 *)(s_ + 8 * th);
 #pragma unroll
-      for (int i = 0; i < 8; i++)
-        x[i] = s_[th + 256 * i];
+      for (int i = 0; i < 4; i++) {
+        const ulonglong2 w = v2[i];
+        x[2 * i] = w.x;
+        x[2 * i + 1] = w.y;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 8; k++)
@@ -2462,16 +2467,10 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         __syncthreads();  // the previous phase has finished with the LDS tile
         if (j ? nat1 : nat0) {
 #pragma unroll
-          for (int i = 0; i < 8; i++) {
-            const int e = th + 256 * i;
-            lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = xn[j][i];
-          }
+          for (int k = 0; k < 8; k++)
+            r[k] = A::load(xn[j][k]);
           if (p + 1 < p1)
             fetch(xn[j], j, p + 1);  // prefetch: in flight during the rest of this ciphertext
-          __syncthreads();
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            r[k] = A::load(lds[T::at(row, 8 * h + k)]);
         } else {
 #pragma unroll
           for (int k = 0; k < 8; k++)
@@ -2529,20 +2528,18 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          __syncthreads();
+          const ulonglong2 *v2 = (const ulonglong2 *)(c0 + ((size_t)half * lvl << logn) + 8 * th);
 #pragma unroll
-          for (int i = 0; i < 8; i++) {
-            const int e = th + 256 * i;
-            lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = c0[((size_t)half * lvl << logn) + e];
-          }
-          __syncthreads();
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const uint64_t c = mul_shoup(lds[T::at(row, 8 * h + k)], mc.pmod, mc.pmodp, q);
-            if (half)
-              a1[k] = add_mod(a1[k], c, q);
-            else
-              a0[k] = add_mod(a0[k], c, q);
+          for (int i = 0; i < 4; i++) {
+            const ulonglong2 w = v2[i];
+            const uint64_t cl = mul_shoup(w.x, mc.pmod, mc.pmodp, q), ch = mul_shoup(w.y, mc.pmod, mc.pmodp, q);
+            if (half) {
+              a1[2 * i] = add_mod(a1[2 * i], cl, q);
+              a1[2 * i + 1] = add_mod(a1[2 * i + 1], ch, q);
+            } else {
+              a0[2 * i] = add_mod(a0[2 * i], cl, q);
+              a0[2 * i + 1] = add_mod(a0[2 * i + 1], ch, q);
+            }
           }
         }
       }
@@ -2554,17 +2551,10 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
       } else if (t < drop_lo || (ablate & 8)) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          __syncthreads();
+          ulonglong2 *d2 = (ulonglong2 *)((half ? o1 : o0) + 8 * th);
 #pragma unroll
-          for (int k = 0; k < 8; k++)
-            lds[T::at(row, 8 * h + k)] = half ? a1[k] : a0[k];
-          __syncthreads();
-          uint64_t *dst = half ? o1 : o0;
-#pragma unroll
-          for (int i = 0; i < 8; i++) {
-            const int e = th + 256 * i;
-            dst[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
-          }
+          for (int i = 0; i < 4; i++)
+            d2[i] = half ? make_ulonglong2(a1[2 * i], a1[2 * i + 1]) : make_ulonglong2(a0[2 * i], a0[2 * i + 1]);
         }
       } else {
         // limb dropped by the following ModDown: inverse row pass (dn_cols
