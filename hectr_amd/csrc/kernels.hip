@@ -3102,14 +3102,19 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
   {
     // reads the nd row-transformed drop limbs, writes keep column-transformed limbs
     ProfScope ps(KC_DN_COLS, 8.0 * n * npoly * (tab.nd + keep));
-    constexpr unsigned NT = 8;  // one block per (poly, tile): the INTT columns are not recomputed
-    const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
-    if (tab.nd <= 4)
-      hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+    // NT = 8: one block per (poly, tile), the INTT columns run once; NT = 4
+    // (GPQHE_DN_NT=4): twice the blocks, the INTT columns run twice
+    static const unsigned nt = getenv("GPQHE_DN_NT") ? atoi(getenv("GPQHE_DN_NT")) : 8;
+    constexpr unsigned NT = 8;
+    const unsigned members = (keep + nt - 1) / nt, ngroups = npoly * tiles;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, conv,
+                         G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+    };
+    if (nt == 4)
+      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, 4, false>) : go(dn_cols_kernel<LOGT1, 4, true>);
     else
-      hipLaunchKernelGGL((dn_cols_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, X, x_pstride, conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false>) : go(dn_cols_kernel<LOGT1, NT, true>);
   }
   // reads conv, X and d01 keep limbs, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
