@@ -226,3 +226,53 @@ def test_batch_real_encryptions_decode(product):
         got = product.decrypt(ct, sk)
         assert np.abs(got - za[i] * zb[i]).max() < 1e-6
         product.free(ct)
+
+
+@pytest.mark.parametrize("name,lvl,cnt", [("bench51", 6, 2), ("bench_d2", 3, 2), ("bench51", 8, 1),
+                                          ("bench51", 8, 0)])
+def test_mul_rescale_batch_levels(oracle, product, name, lvl, cnt):
+    """The fused batch op below the top level (lvl 6: digits {0..3} {4,5},
+    a partial digit; lvl 3: one partial digit), a batch of one pair and an
+    empty batch (a no-op that must not touch the output)."""
+    import ctypes
+    import torch
+    init_both(oracle, product, name)
+    n = product.n
+    _, _, _, rlk_o = keys(oracle, rot=False)
+    _, _, _, rlk_p = keys(product, rot=False)
+    words = max(cnt, 1) * 2 * lvl * n
+    a = np.zeros(words, dtype=np.uint64)
+    b = np.zeros(words, dtype=np.uint64)
+    oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * max(cnt, 1), lvl, 5)
+    oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * max(cnt, 1), lvl, 6)
+    out_o = np.full(max(cnt, 1) * 2 * (lvl - 1) * n, 7, dtype=np.uint64)
+    oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, lvl, ctypes.byref(rlk_o))
+    da = torch.from_numpy(a.view(np.int64)).cuda()
+    db = torch.from_numpy(b.view(np.int64)).cuda()
+    dout = torch.full((out_o.size,), 7, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, lvl, ctypes.byref(rlk_p))
+    product.sync()
+    got = dout.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, out_o), f"{np.count_nonzero(got != out_o)} residues differ"
+    if cnt == 0:
+        assert np.all(got == 7)
+
+
+def test_gemv_zero_matrix(oracle, product):
+    """he_gemv with an all-zero matrix (no diagonal is launched): the output is
+    an encryption of zero, bit-exact with the oracle."""
+    init_both(oracle, product, "ref")
+    res = {}
+    z = np.linspace(-1, 1, oracle.slots) + 0j
+    M = np.zeros((oracle.slots, oracle.slots))
+    for e in (oracle, product):
+        pk, sk, rk, _ = keys(e)
+        x = e.encrypt(z, pk)
+        y = e.ct()
+        e.gemv(y, M.ravel(), x, rk)
+        res[e.name] = (e, y, sk)
+    same(oracle, product, res["oracle"][1], res["product"][1])
+    e, y, sk = res["product"]
+    assert np.abs(e.decrypt(y, sk)).max() < 1e-6
+
