@@ -67,8 +67,12 @@ def main():
     from hectr_amd.gpqhe import Engine
 
     rank, world, local = hdist.env()
-    torch.cuda.set_device(local)
-    hdist.init("nccl")
+    # one process per GPU; the modulus only matters for rehearsals with more
+    # ranks than GPUs (HECTR_DIST_BACKEND=gloo: RCCL needs distinct devices)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    backend = os.environ.get("HECTR_DIST_BACKEND", "nccl")
+    hdist.init(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
     barrier = hdist.barrier
 
     L, logn, B = args.nlimbs, args.logn, args.batch
@@ -113,7 +117,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     ev_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = hdist.max_over_ranks(elapsed, device="cuda")
+    elapsed = hdist.max_over_ranks(elapsed, device=red_dev)
     ops = world * B * args.steps
     value = ops / elapsed
     ms_per_step = 1e3 * elapsed / args.steps

@@ -25,7 +25,7 @@ def init(backend: str):
         kw = {}
         if backend == "nccl":
             import torch
-            kw["device_id"] = torch.device("cuda", local)
+            kw["device_id"] = torch.device("cuda", local % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend, **kw)
     return rank, world, local
 
