@@ -201,7 +201,11 @@ def pmc_traffic(kernel, workload):
     the gfx950 FETCH_SIZE x2 correction).  (None, None) when no profile of this
     workload exists: PMC counters cannot be read from inside the timed run."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime, reverse=True)
+    import re
+    def order(f):  # profiles/r<round>_v<version>_pmc.json, newest first
+        m = re.search(r"r(\d+)_v(\d+)_pmc", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order, reverse=True)
     for f in files:
         try:
             d = json.load(open(f))
