@@ -497,6 +497,22 @@ __device__ __forceinline__ double f64_red(double x, double q, double qinv)
   return __fma_rn(-rint(x * qinv), q, x);
 }
 
+// u64 <-> f64 for integers below 2^52 without the generic conversions (4 and
+// ~7 instructions): 2^52 + x has x as its mantissa bits.
+__device__ __forceinline__ double f64_from_u52(uint64_t x)
+{
+  return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 0x1p52;
+}
+
+// canonical residue of x (integer, |x| < 2^53): reduce, lift negatives by
+// q and read the mantissa of 2^52 + v
+__device__ __forceinline__ uint64_t f64_canon(double x, double q, double qinv)
+{
+  const double v = f64_red(x, q, qinv);
+  const double b = v < 0 ? q + 0x1p52 : 0x1p52;
+  return (uint64_t)__double_as_longlong(v + b) & ((1ull << 52) - 1);
+}
+
 template <int LE>
 __device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
                                              int log_thi, double q, double qinv)
@@ -564,13 +580,8 @@ struct ArF64 {
   double q, qinv;
   const double *tw;   // this modulus' forward (w, w / q) pairs
   const double *itw;  // and inverse
-  __device__ static V load(uint64_t x) { return (double)x; }
-  __device__ uint64_t canon(V x) const
-  {
-    double v = f64_red(x, q, qinv);
-    v = v < 0 ? v + q : v;
-    return (uint64_t)v;
-  }
+  __device__ static V load(uint64_t x) { return f64_from_u52(x); }  // x canonical (< q)
+  __device__ uint64_t canon(V x) const { return f64_canon(x, q, qinv); }
   __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
   __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
   template <int LE>
@@ -585,7 +596,7 @@ struct ArF64 {
   }
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
   {
-    const double wd = (double)w;
+    const double wd = f64_from_u52(w);
     return canon(f64_mulmod(x, wd, wd / q, q));
   }
 };
@@ -1300,31 +1311,57 @@ void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t ps)
 }
 
 // Tensor of count ciphertext pairs: d0 = a0 b0, d1 = a0 b1 + a1 b0 into
-// d01 [count][2][lvl][n]; d2 = a1 b1 into d2 [count][lvl][n].
-__global__ void tensor_kernel(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b, unsigned logn,
-                              unsigned lvl, size_t in_stride, size_t in_pstride, size_t d01_stride, size_t d2_stride,
-                              const ModConst *mc)
+// d01 [count][2][lvl][n]; d2 = a1 b1 into d2 [count][lvl][n].  Two adjacent
+// coefficients per thread (16-byte accesses).  Moduli below 2^51 use the exact
+// FP64 product (f64_mulmod with a variable second operand: both factors < q,
+// so ab / q < 2^51, the quotient estimate is off by < 1.25 and every
+// intermediate is an integer below 2^53); wider moduli use Barrett.
+__global__ void __launch_bounds__(256) tensor_kernel(uint64_t *d01, uint64_t *d2, const uint64_t *a,
+                                                     const uint64_t *b, unsigned logn, unsigned lvl, size_t in_stride,
+                                                     size_t in_pstride, size_t d01_stride, size_t d2_stride,
+                                                     const ModConst *mc)
 {
   const size_t n = (size_t)1 << logn;
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = 2 * ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
   const unsigned limb = blockIdx.y, c = blockIdx.z;
   if (i >= n)
     return;
   const ModConst m = mc[limb];
   const size_t off = ((size_t)limb << logn) + i;
   const uint64_t *pa = a + c * in_stride, *pb = b + c * in_stride;
-  const uint64_t a0 = pa[off], a1 = pa[in_pstride + off], b0 = pb[off], b1 = pb[in_pstride + off];
+  const ulonglong2 A0 = *(const ulonglong2 *)(pa + off), A1 = *(const ulonglong2 *)(pa + in_pstride + off);
+  const ulonglong2 B0 = *(const ulonglong2 *)(pb + off), B1 = *(const ulonglong2 *)(pb + in_pstride + off);
+  uint64_t r0[2], r1[2], r2[2];
+  const uint64_t a0[2] = {A0.x, A0.y}, a1[2] = {A1.x, A1.y}, b0[2] = {B0.x, B0.y}, b1[2] = {B1.x, B1.y};
+  if (m.q < F64_QMAX) {
+    const double q = (double)m.q, qinv = 1.0 / q;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const double x0 = f64_from_u52(a0[e]), x1 = f64_from_u52(a1[e]);
+      const double y0 = f64_from_u52(b0[e]), y1 = f64_from_u52(b1[e]);
+      r0[e] = f64_canon(f64_mulmod(x0, y0, y0 * qinv, q), q, qinv);
+      r1[e] = f64_canon(f64_mulmod(x0, y1, y1 * qinv, q) + f64_mulmod(x1, y0, y0 * qinv, q), q, qinv);
+      r2[e] = f64_canon(f64_mulmod(x1, y1, y1 * qinv, q), q, qinv);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      r0[e] = mul_mod(a0[e], b0[e], m);
+      r1[e] = add_mod(mul_mod(a0[e], b1[e], m), mul_mod(a1[e], b0[e], m), m.q);
+      r2[e] = mul_mod(a1[e], b1[e], m);
+    }
+  }
   uint64_t *o = d01 + c * d01_stride;
-  o[off] = mul_mod(a0, b0, m);
-  o[((size_t)lvl << logn) + off] = add_mod(mul_mod(a0, b1, m), mul_mod(a1, b0, m), m.q);
-  d2[c * d2_stride + off] = mul_mod(a1, b1, m);
+  *(ulonglong2 *)(o + off) = make_ulonglong2(r0[0], r0[1]);
+  *(ulonglong2 *)(o + ((size_t)lvl << logn) + off) = make_ulonglong2(r1[0], r1[1]);
+  *(ulonglong2 *)(d2 + c * d2_stride + off) = make_ulonglong2(r2[0], r2[1]);
 }
 
 void k_tensor(uint64_t *d01, uint64_t *d2c, const uint64_t *a, const uint64_t *b, unsigned lvl,
               size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride)
 {
   ProfScope ps(KC_TENSOR, 8.0 * G.n * lvl * count * 7);  // read 4 limbs, write 3 limbs
-  hipLaunchKernelGGL(tensor_kernel, dim3((G.n + TPB - 1) / TPB, lvl, count), dim3(TPB), 0, G.stream, d01, d2c, a,
+  hipLaunchKernelGGL(tensor_kernel, dim3((G.n / 2 + TPB - 1) / TPB, lvl, count), dim3(TPB), 0, G.stream, d01, d2c, a,
                      b, G.logn, lvl, in_stride, in_pstride, d_stride, (size_t)lvl << G.logn, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
