@@ -573,6 +573,7 @@ struct ArInt {
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, itw, bb, log_tlo, q); }
   // canonical x w for a constant w < q (Shoup pair)
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
+  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t wp) const { return mulc(x, w, wp); }  // (FP64 only)
 };
 
 struct ArF64 {
@@ -599,7 +600,24 @@ struct ArF64 {
     const double wd = f64_from_u52(w);
     return canon(f64_mulmod(x, wd, wd / q, q));
   }
+  // x w as the bits of a canonical double in [0, q) (FP64 basis conversion input)
+  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t) const
+  {
+    const double wd = f64_from_u52(w);
+    const double v = f64_red(f64_mulmod(x, wd, wd / q, q), q, qinv);
+    return (uint64_t)__double_as_longlong(v < 0 ? v + q : v);
+  }
 };
+
+// FP64 fast basis conversion term y c mod q_t for canonical y < q_i < 2^51 and
+// a constant c < q_t < 2^51 with cq = fl(c / q_t): y c / q_t < 2^51, so the
+// quotient estimate is off by at most 1, |result| <= q_t and every
+// intermediate is an integer below 2^53 (exact).  Sums of up to three terms
+// stay below 2^53; longer sums are reduced in between (f64_red).
+__device__ __forceinline__ double fbc_term(double y, double c, double cq, double q)
+{
+  return f64_mulmod(y, c, cq, q);
+}
 
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
 
@@ -618,6 +636,27 @@ __device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn
     f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
   else
     f(ArInt{q, tw.fwd + o, tw.inv + o});
+}
+
+// FP64 basis conversion per kernel (GPQHE_FBC64 bit mask, timing studies):
+// 1 ks_cols4, 2 dn_cols.  Both are exact; the mask only selects the faster one.
+static int fbc64_mask()
+{
+  static const int m = getenv("GPQHE_FBC64") ? atoi(getenv("GPQHE_FBC64")) : 2;
+  return m;
+}
+
+// with_arith for kernels instantiated per prime set: ALL_F64 (every modulus
+// < 2^51, FP64 tables present) keeps only the FP64 policy in the code.
+template <bool ALL_F64, class F>
+__device__ __forceinline__ void with_arith_t(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
+{
+  if constexpr (ALL_F64) {
+    const size_t o = (size_t)m << (logn + 1);
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+  } else {
+    with_arith(q, m, logn, tw, f);
+  }
 }
 
 // Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
@@ -1672,7 +1711,9 @@ struct UpTable {
   uint64_t *ysc;  // [lvl][2]       n^-1 [(Qj/q_i)^-1]_{q_i} + Shoup (folded into the INTT)
   uint64_t *ysc1; // [lvl][2]       n1^-1 [(Qj/q_i)^-1]_{q_i}: INTT columns after tensor_rows
   uint64_t *n2i;  // [lvl][2]       n2^-1 mod q_i (tensor_rows output scale)
+  double *cd;     // [ndig][8][nm][2] ([Qj/q_i]_t, that / q_t) as doubles (FP64 conversion)
   unsigned ndig, nm;
+  int f64;        // every modulus of the basis < 2^51 (and FP64 enabled): FP64 conversion
 };
 
 // Row length n2 of the fused kernels' 4-step split (n = n1 x n2).
@@ -1695,6 +1736,7 @@ static UpTable &up_table(unsigned lvl)
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha;
   std::vector<UpDigit> dig(ndig);
   std::vector<uint64_t> c((size_t)ndig * 8 * nm, 0);
+  std::vector<double> cd((size_t)ndig * 8 * nm * 2, 0.0);
   for (unsigned j = 0; j < ndig; j++) {
     const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, lvl);
     dig[j].lo = lo;
@@ -1713,6 +1755,8 @@ static UpTable &up_table(unsigned lvl)
           if (i2 != i)
             h = hm_mul_mod(h, G.q[i2] % qt, qt);
         c[((size_t)j * 8 + (i - lo)) * nm + t] = hm_mul_mod(h, G.mc[mods[t]].r64, qt);  // Montgomery form
+        cd[2 * (((size_t)j * 8 + (i - lo)) * nm + t)] = (double)h;
+        cd[2 * (((size_t)j * 8 + (i - lo)) * nm + t) + 1] = (double)h / (double)qt;
       }
     }
   }
@@ -1738,6 +1782,11 @@ static UpTable &up_table(unsigned lvl)
   UpTable tab;
   tab.ndig = ndig;
   tab.nm = nm;
+  tab.f64 = G.twd != nullptr;
+  for (unsigned t = 0; t < nm; t++)
+    tab.f64 &= G.q[mods[t]] < (1ull << 51);
+  HIP_CHECK(hipMalloc(&tab.cd, cd.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.cd, cd.data(), cd.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
   HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.ysc1, ysc1.size() * 8));
@@ -2106,7 +2155,7 @@ __global__ void __launch_bounds__(256) tensor_rows_kernel(uint64_t *d01, size_t 
 // targets in turn (the single-target kernel re-reads them through L2 for every
 // target and waits on those loads most of its time).  Column tiles are double
 // buffered in LDS, so one barrier per target suffices.
-template <int LOGT, int NT, bool INVC>
+template <int LOGT, int NT, bool INVC, bool F64>
 __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
                                                            size_t t1_stride, unsigned logn, unsigned lvl,
                                                            unsigned L, unsigned nm, unsigned ndig, unsigned members,
@@ -2135,8 +2184,10 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
 #pragma unroll
       for (int i = 0; i < 4; i++)
 #pragma unroll
-        for (int k = 0; k < EA; k++)
-          y[it][i][k] = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+        for (int k = 0; k < EA; k++) {
+          const uint64_t v = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+          y[it][i][k] = F64 ? (uint64_t)__double_as_longlong(f64_from_u52(v)) : v;
+        }
     }
   } else {
     // the digit arrives after the inverse row pass (tensor_rows_kernel): run
@@ -2156,7 +2207,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       const uint64_t *src = yb + ((size_t)i << logn);
       if (i)
         __syncthreads();
-      with_arith(mcs[mi_].q, mi_, logn, tw, [&](const auto &ar) {
+      with_arith_t<F64>(mcs[mi_].q, mi_, logn, tw, [&](const auto &ar) {
         using A = std::decay_t<decltype(ar)>;
         using V = typename A::V;
         {
@@ -2181,7 +2232,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
           ar.template inv<LEA>(r, T, 4);
 #pragma unroll
           for (int k = 0; k < EA; k++)
-            y[it][i][k] = ar.mulc(r[k], w, wp);
+            y[it][i][k] = F64 ? ar.mulc_d(r[k], w, wp) : ar.mulc(r[k], w, wp);
         }
       });
     };
@@ -2205,20 +2256,41 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       cc[i] = i < (int)na ? tab.c[((size_t)j * 8 + i) * nm + t] : 0;
     uint64_t *buf = lds[u & 1];
     uint64_t *out = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + (size_t)tile * C;
-    with_arith(q, m, logn, tw, [&](const auto &ar) {
+    with_arith_t<F64>(q, m, logn, tw, [&](const auto &ar) {
       using A = std::decay_t<decltype(ar)>;
       using V = typename A::V;
 #pragma unroll
       for (int it = 0; it < IT; it++) {
         const int item = th + 256 * it, c = item % C, l = item / C;
         V r[EA];
+        bool done = false;
+        if constexpr (F64 && std::is_same<A, ArF64>::value) {
+          {
+            double cw[4], cq[4];
 #pragma unroll
-        for (int k = 0; k < EA; k++) {
-          unsigned __int128 acc = 0;
+            for (int i = 0; i < 4; i++) {
+              cw[i] = i < (int)na ? tab.cd[2 * (((size_t)j * 8 + i) * nm + t)] : 0.0;
+              cq[i] = i < (int)na ? tab.cd[2 * (((size_t)j * 8 + i) * nm + t) + 1] : 0.0;
+            }
 #pragma unroll
-          for (int i = 0; i < 4; i++)
-            acc += (unsigned __int128)y[it][i][k] * cc[i];
-          r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+            for (int k = 0; k < EA; k++) {
+              auto yd = [&](int i) { return __longlong_as_double((long long)y[it][i][k]); };
+              const double v = fbc_term(yd(0), cw[0], cq[0], ar.q) + fbc_term(yd(1), cw[1], cq[1], ar.q) +
+                               fbc_term(yd(2), cw[2], cq[2], ar.q);
+              r[k] = f64_red(v, ar.q, ar.qinv) + fbc_term(yd(3), cw[3], cq[3], ar.q);  // |.| < 1.5 q
+            }
+            done = true;
+          }
+        }
+        if (!done) {
+#pragma unroll
+          for (int k = 0; k < EA; k++) {
+            unsigned __int128 acc = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              acc += (unsigned __int128)y[it][i][k] * cc[i];
+            r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+          }
         }
         ar.template fwd<LEA>(r, T, LOGT - 1);
 #pragma unroll
@@ -2636,16 +2708,22 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
       constexpr unsigned NT = 8;  // all targets of a digit tile: its INTT columns run once
       const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
-      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, true>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
-                         tw, G.dev.mc);
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
+                           t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
+      };
+      tab.f64 && (fbc64_mask() & 1) ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
+                                    : go(ks_cols4_kernel<LOGT1, NT, true, false>);
     } else if (G.alpha <= 4) {
       constexpr unsigned NT = 4;
       const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
-      hipLaunchKernelGGL((ks_cols4_kernel<LOGT1, NT, false>), dim3(xcd_blocks(members, ngroups)), dim3(256), 0,
-                         G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab,
-                         tw, G.dev.mc);
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
+                           t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
+      };
+      tab.f64 && (fbc64_mask() & 1) ? go(ks_cols4_kernel<LOGT1, NT, false, true>)
+                                    : go(ks_cols4_kernel<LOGT1, NT, false, false>);
     } else {
       hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
@@ -2767,7 +2845,9 @@ struct DownTable {
   uint64_t *y, *yp;  // [nd]        [(Dprod/d)^-1]_d
   uint64_t *c;       // [nd][keep]  [Dprod/d]_t
   uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
+  double *cd;        // [nd][keep][2] ([Dprod/d]_t, that / q_t) as doubles (FP64 conversion)
   unsigned keep, nd;
+  int f64;           // every modulus < 2^51 (and FP64 enabled): FP64 conversion
 };
 
 static std::map<std::pair<unsigned, int>, DownTable> g_down;
@@ -2788,6 +2868,7 @@ static DownTable &down_table(unsigned lvl, int mode)
       mods[t] = t;
   const unsigned keep = mode == 0 ? lvl : lvl - 1, nd = nm - keep;
   std::vector<uint64_t> y(nd), yp(nd), c((size_t)nd * keep), dinv(keep), dinvp(keep);
+  std::vector<double> cd((size_t)nd * keep * 2);
   for (unsigned d = 0; d < nd; d++) {
     const uint64_t qd = G.q[mods[keep + d]];
     uint64_t hat = 1;
@@ -2803,6 +2884,8 @@ static DownTable &down_table(unsigned lvl, int mode)
         if (d2 != d)
           h = hm_mul_mod(h, G.q[mods[keep + d2]] % qt, qt);
       c[(size_t)d * keep + t] = hm_mul_mod(h, G.mc[mods[t]].r64, qt);  // Montgomery form
+      cd[2 * ((size_t)d * keep + t)] = (double)h;
+      cd[2 * ((size_t)d * keep + t) + 1] = (double)h / (double)qt;
     }
   }
   for (unsigned t = 0; t < keep; t++) {
@@ -2831,6 +2914,11 @@ static DownTable &down_table(unsigned lvl, int mode)
   DownTable tab;
   tab.keep = keep;
   tab.nd = nd;
+  tab.f64 = G.twd != nullptr;
+  for (unsigned t = 0; t < nm; t++)
+    tab.f64 &= G.q[mods[t]] < (1ull << 51);
+  HIP_CHECK(hipMalloc(&tab.cd, cd.size() * 8));
+  HIP_CHECK(hipMemcpy(tab.cd, cd.data(), cd.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
   HIP_CHECK(hipMalloc(&tab.fin, fin.size() * 8));
   HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
@@ -2945,7 +3033,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 // The converted polynomial never reaches HBM in coefficient form and the
 // combine is the row pass's epilogue.
 // ===========================================================================
-template <int LOGT, int NT, bool X5>
+template <int LOGT, int NT, bool X5, bool F64>
 __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, uint64_t *conv,
                                                           unsigned logn, unsigned lvl, unsigned L, unsigned members,
                                                           unsigned ngroups, DownTable tab, Tw2 tw,
@@ -2978,7 +3066,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
     const uint64_t *src = yb + ((size_t)d << logn);
     if (d)
       __syncthreads();
-    with_arith(mcs[md].q, md, logn, tw, [&](const auto &ar) {
+    with_arith_t<F64>(mcs[md].q, md, logn, tw, [&](const auto &ar) {
       using A = std::decay_t<decltype(ar)>;
       using V = typename A::V;
       {
@@ -3003,7 +3091,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
         ar.template inv<LEA>(r, T, 4);
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          const uint64_t v = ar.mulc(r[k], w, wp);
+          const uint64_t v = F64 ? ar.mulc_d(r[k], w, wp) : ar.mulc(r[k], w, wp);
           if (d < 4)
             y[it][d < 4 ? d : 0][k] = v;
           else if constexpr (X5)
@@ -3035,22 +3123,49 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
     if (u)
       __syncthreads();  // the previous target's round B has read the tile
     uint64_t *out = conv + (((size_t)p * keep + t) << logn) + (size_t)tile * C;
-    with_arith(q, m, logn, tw, [&](const auto &ar) {
+    with_arith_t<F64>(q, m, logn, tw, [&](const auto &ar) {
       using A = std::decay_t<decltype(ar)>;
       using V = typename A::V;
 #pragma unroll
       for (int it = 0; it < IT; it++) {
         const int item = th + 256 * it, c = item % C, l = item / C;
         V r[EA];
+        bool done = false;
+        if constexpr (F64 && std::is_same<A, ArF64>::value) {
+          {
+            // FP64 conversion: sources are canonical doubles, constants plain
+            double cw[5], cq[5];
 #pragma unroll
-        for (int k = 0; k < EA; k++) {
-          unsigned __int128 acc = 0;
+            for (int d = 0; d < 5; d++) {
+              cw[d] = d < (int)nd ? tab.cd[2 * ((size_t)d * keep + t)] : 0.0;
+              cq[d] = d < (int)nd ? tab.cd[2 * ((size_t)d * keep + t) + 1] : 0.0;
+            }
 #pragma unroll
-          for (int d = 0; d < 4; d++)
-            acc += (unsigned __int128)y[it][d][k] * cc[d];
-          if constexpr (X5)
-            acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
-          r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+            for (int k = 0; k < EA; k++) {
+              auto yd = [&](int d) { return __longlong_as_double((long long)y[it][d][k]); };
+              double v = fbc_term(yd(0), cw[0], cq[0], ar.q) + fbc_term(yd(1), cw[1], cq[1], ar.q) +
+                         fbc_term(yd(2), cw[2], cq[2], ar.q);
+              v = f64_red(v, ar.q, ar.qinv) + fbc_term(yd(3), cw[3], cq[3], ar.q);
+              if constexpr (X5)
+                v = f64_red(v + fbc_term(__longlong_as_double((long long)y5[(it * EA + k) * 256 + th]), cw[4],
+                                         cq[4], ar.q),
+                            ar.q, ar.qinv);
+              r[k] = v;  // |v| < 2 q
+            }
+            done = true;
+          }
+        }
+        if (!done) {
+#pragma unroll
+          for (int k = 0; k < EA; k++) {
+            unsigned __int128 acc = 0;
+#pragma unroll
+            for (int d = 0; d < 4; d++)
+              acc += (unsigned __int128)y[it][d][k] * cc[d];
+            if constexpr (X5)
+              acc += (unsigned __int128)y5[(it * EA + k) * 256 + th] * cc[4];
+            r[k] = A::load(redc128((uint64_t)(acc >> 64), (uint64_t)acc, mc));
+          }
         }
         ar.template fwd<LEA>(r, T, LOGT - 1);
 #pragma unroll
@@ -3148,10 +3263,17 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
       hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, conv,
                          G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     };
+    auto go2 = [&](auto nt_c) {
+      constexpr unsigned N = decltype(nt_c)::value;
+      if (tab.f64 && (fbc64_mask() & 2))
+        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, N, false, true>) : go(dn_cols_kernel<LOGT1, N, true, true>);
+      else
+        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, N, false, false>) : go(dn_cols_kernel<LOGT1, N, true, false>);
+    };
     if (nt == 4)
-      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, 4, false>) : go(dn_cols_kernel<LOGT1, 4, true>);
+      go2(std::integral_constant<unsigned, 4>{});
     else
-      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false>) : go(dn_cols_kernel<LOGT1, NT, true>);
+      go2(std::integral_constant<unsigned, NT>{});
   }
   // reads conv, X and d01 keep limbs, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
@@ -3292,6 +3414,7 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.ysc));
     HIP_CHECK(hipFree(kv.second.ysc1));
     HIP_CHECK(hipFree(kv.second.n2i));
+    HIP_CHECK(hipFree(kv.second.cd));
   }
   g_up.clear();
   for (auto &kv : g_down) {
@@ -3302,6 +3425,7 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.dinvp));
     HIP_CHECK(hipFree(kv.second.ysc));
     HIP_CHECK(hipFree(kv.second.fin));
+    HIP_CHECK(hipFree(kv.second.cd));
   }
   g_down.clear();
 }
