@@ -182,8 +182,9 @@ static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
   o->npoly = npoly;
   o->cap = cap;
   const size_t bytes = ((size_t)npoly * cap << G.logn) * 8;
+  // No zero fill: a fresh object has nlimbs = 0, and every read of an object
+  // is bounded by its nlimbs, so its payload is written before it is read.
   o->data = (uint64_t *)pool_alloc(bytes);
-  HIP_CHECK(hipMemsetAsync(o->data, 0, bytes, G.stream));
 }
 
 static void obj_free(void *vo)
@@ -615,8 +616,7 @@ static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scal
   Ws dcoef(G.n);
   upload(dcoef.p, coef.data(), (size_t)G.n * 8);
   LimbSet ls = limbset(dst, mods, nm, 1, (size_t)nm << G.logn);
-  k_lift_i64(ls, (const int64_t *)dcoef.p);
-  k_ntt(ls, false);
+  k_lift_ntt(ls, (const int64_t *)dcoef.p);
 }
 
 extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int slots, double scale,

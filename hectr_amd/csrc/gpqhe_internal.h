@@ -248,6 +248,7 @@ void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);
 void k_lift_i64(const LimbSet &dst, const int64_t *coef);
+void k_lift_ntt(const LimbSet &dst, const int64_t *coef);  // lift + forward NTT
 void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
                    const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl);
 void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,

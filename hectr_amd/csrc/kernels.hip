@@ -1141,8 +1141,20 @@ void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_
 // butterflies on the limb's arithmetic policy.  Round r covers global stages
 // [3r, 3r + 3): thread t's group starts at pos0 = (t / D8) 8 D8 + t % D8 with
 // D8 = n >> (3r + 3) the group's smallest distance, twiddle base n + pos0.
+// coef != nullptr (forward only): round 0 reads the signed integer
+// coefficients shared by every limb and lifts them mod q (encoding), instead
+// of a separate lift launch.
+__device__ __forceinline__ uint64_t lift_i64(int64_t v, const ModConst &c)
+{
+  if (v >= 0)
+    return reduce64((uint64_t)v, c);
+  const uint64_t r = reduce64((uint64_t)(-(v + 1)), c) + 1;  // |v| mod q in [1, q]
+  return r == c.q ? 0 : c.q - r;
+}
+
 template <int LOGN, bool INV>
-__global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs)
+__global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs,
+                                                         const int64_t *coef)
 {
   constexpr int n = 1 << LOGN, NT = n / 8, FULL = LOGN / 3, REM = LOGN % 3;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
@@ -1167,7 +1179,8 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
         group(r, pos0, d8);
 #pragma unroll
         for (int k = 0; k < 8; k++)
-          a[k] = r ? A::unbits(lds[pos0 + k * d8]) : A::load(x[pos0 + k * d8]);
+          a[k] = r ? A::unbits(lds[pos0 + k * d8])
+                   : A::load(coef ? lift_i64(coef[pos0 + k * d8], mc) : x[pos0 + k * d8]);
         ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
         if (r + 1 < FULL || REM) {
 #pragma unroll
@@ -1244,6 +1257,29 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
   (void)NT;
 }
 
+// Encoding: lift the signed coefficients into every limb of s, then the
+// forward NTT (one launch for n <= 2^12).
+void k_lift_ntt(const LimbSet &s, const int64_t *coef)
+{
+  if (G.logn >= 10 && G.logn <= 12 && !getenv("GPQHE_NTT_WHOLE_V1")) {
+    ProfScope ps(KC_NTT_SMALL_FWD, 8.0 * G.n * (s.count + 1));
+    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+    auto go = [&](auto kern, unsigned threads) {
+      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, coef);
+    };
+    if (G.logn == 12)
+      go(ntt_small_kernel<12, false>, 512);
+    else if (G.logn == 11)
+      go(ntt_small_kernel<11, false>, 256);
+    else
+      go(ntt_small_kernel<10, false>, 128);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
+  k_lift_i64(s, coef);
+  k_ntt(s, false);
+}
+
 void k_ntt(const LimbSet &s, bool inverse)
 {
   if (!s.count)
@@ -1255,7 +1291,7 @@ void k_ntt(const LimbSet &s, bool inverse)
     ProfScope ps(inverse ? KC_NTT_SMALL_INV : KC_NTT_SMALL_FWD, 16.0 * n * s.count);
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern, unsigned threads) {
-      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc);
+      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, (const int64_t *)nullptr);
     };
     if (logn == 12)
       inverse ? go(ntt_small_kernel<12, true>, 512) : go(ntt_small_kernel<12, false>, 512);
@@ -1519,13 +1555,7 @@ __global__ void lift_i64_kernel(LimbSet dst, const int64_t *coef, unsigned logn,
     return;
   const unsigned l = blockIdx.y;
   const ModConst c = mc[dst.mod(l)];
-  const int64_t v = coef[k];
-  uint64_t r;
-  if (v >= 0)
-    r = reduce64((uint64_t)v, c);
-  else
-    r = neg_mod(reduce64((uint64_t)(-(v + 1)), c) + 1 == c.q ? 0 : reduce64((uint64_t)(-(v + 1)), c) + 1, c.q);
-  dst.limb(l, logn)[k] = r;
+  dst.limb(l, logn)[k] = lift_i64(coef[k], c);
 }
 
 void k_lift_i64(const LimbSet &dst, const int64_t *coef)

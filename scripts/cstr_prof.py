@@ -9,12 +9,13 @@ from hectr_amd.cstr import CstrProblem, EncryptedRegulator
 from hectr_amd.gpqhe import Engine
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+prof = not (len(sys.argv) > 2 and sys.argv[2] == "noprof")  # noprof: for rocprofv3 --kernel-trace
 pb = CstrProblem(steps)
 eng = Engine.product()
 reg = EncryptedRegulator(eng, pb, seed=5)
 pb.simulate(reg)  # warm: diagonal cache, pool, code objects
 reg.timings.clear()
-eng.prof_enable(True)
+eng.prof_enable(prof)
 t0 = time.perf_counter()
 x, u = pb.simulate(reg)
 dt = time.perf_counter() - t0
