@@ -860,6 +860,27 @@ __global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, LimbSet o, un
 // column c of row r sits at c ^ ((c >> 3) & (TA - 1)) (^ (r & 1) << 4 for
 // N2 = 128).
 // ---------------------------------------------------------------------------
+// Every exchange of the 8-element row passes stays inside one row, and a
+// row belongs to one wave (TA = N2 / 8 threads per row, 64 / TA rows per
+// wave), so the row passes synchronise per wave, not per block: LDS
+// operations of one wave execute in order, the fences only keep the compiler
+// from moving them across the exchange.  Waves of a block never wait for each
+// other.
+__device__ __forceinline__ void wave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Word i < 8 of this thread in a wave-local coalesced walk over a
+// 2048-element row tile: wave w covers elements [512 w, 512 w + 512), which
+// are exactly its own rows.
+__device__ __forceinline__ int wl_elem(int i)
+{
+  return (threadIdx.x & ~63) * 8 + (threadIdx.x & 63) + 64 * i;
+}
+
 template <int LOGN2>
 struct Row8 {
   static constexpr int N2 = 1 << LOGN2, R = 2048 / N2, TA = N2 / 8, TB = TA / 8, EC = 1 << (LOGN2 - 6);
@@ -890,7 +911,7 @@ __device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *l
     for (int k = 0; k < 8; k++)
       lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   {
     const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
 #pragma unroll
@@ -901,7 +922,7 @@ __device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *l
     for (int k = 0; k < 8; k++)
       lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   const int h = th % T::TA;
 #pragma unroll
   for (int k = 0; k < 8; k++)
@@ -934,7 +955,7 @@ __device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)
     for (int k = 0; k < 8; k++)
       lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   {
     const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
 #pragma unroll
@@ -945,7 +966,7 @@ __device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)
     for (int k = 0; k < 8; k++)
       lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   const int h = th % T::TA;
 #pragma unroll
   for (int k = 0; k < 8; k++)
@@ -990,7 +1011,7 @@ __device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, 
     for (int k = 0; k < 8; k++)
       lds[T::at(row, 8 * h + k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   {
     const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
 #pragma unroll
@@ -1001,7 +1022,7 @@ __device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, 
     for (int k = 0; k < 8; k++)
       lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
   }
-  __syncthreads();
+  wave_sync();
   {
     const int l = th % T::TA;
 #pragma unroll
@@ -1027,28 +1048,28 @@ __device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint6
     uint64_t out[8];
     rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0);
     const int h = th % T::TA;
-    __syncthreads();
+    wave_sync();
 #pragma unroll
     for (int k = 0; k < 8; k++)
       lds[T::at(row, 8 * h + k)] = out[k];
-    __syncthreads();
+    wave_sync();
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      const int e = th + 256 * i;
+      const int e = wl_elem(i);
       y[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
     }
   } else {
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      const int e = th + 256 * i;
+      const int e = wl_elem(i);
       lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = x[e];
     }
-    __syncthreads();
+    wave_sync();
     const int h = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
       r[k] = A::load(lds[T::at(row, 8 * h + k)]);
-    __syncthreads();
+    wave_sync();
     rows8_inv<LOGN2>(r, lds, ar, rowbase0);
     const int l = th % T::TA;
 #pragma unroll
@@ -2603,7 +2624,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         V r[8];
-        __syncthreads();  // the previous phase has finished with the LDS tile
+        wave_sync();  // the previous phase has finished with the LDS tile
         if (j ? nat1 : nat0) {
 #pragma unroll
           for (int k = 0; k < 8; k++)
@@ -2704,7 +2725,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 #pragma unroll
           for (int k = 0; k < 8; k++)
             r[k] = A::load(half ? a1[k] : a0[k]);
-          __syncthreads();
+          wave_sync();
           rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
           uint64_t *dst = half ? o1 : o0;
 #pragma unroll
@@ -3247,8 +3268,8 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   uint64_t xv[8], dv[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    xv[i] = xs[th + 256 * i];
-    dv[i] = ds[th + 256 * i];
+    xv[i] = xs[wl_elem(i)];
+    dv[i] = ds[wl_elem(i)];
   }
   uint64_t cv[8];
   with_arith(q, m, logn, tw, [&](const auto &ar) {
@@ -3259,16 +3280,16 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
       r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
     rows8_fwd<LOGN2>(r, cv, lds, ar, n1 + row0);
   });
-  __syncthreads();
+  wave_sync();
 #pragma unroll
   for (int k = 0; k < 8; k++)
     lds[T::at(row, 8 * h + k)] = cv[k];
-  __syncthreads();
+  wave_sync();
   const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], f = tab.fin[2 * t], fp = tab.fin[2 * t + 1];
   uint64_t *o = out + p * out_pstride + toff;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const int e = th + 256 * i;
+    const int e = wl_elem(i);
     const uint64_t c = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
     const uint64_t v = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
     o[e] = add_mod(v, mul_shoup(dv[i], f, fp, q), q);
