@@ -3291,8 +3291,16 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   for (int i = 0; i < 8; i++) {
     const int e = wl_elem(i);
     const uint64_t c = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
-    const uint64_t v = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
-    o[e] = add_mod(v, mul_shoup(dv[i], f, fp, q), q);
+    if (q < F64_QMAX) {
+      // exact FP64 products: |X - conv| < q, each product < 1.25 q
+      const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv), fd = f64_from_u52(f);
+      const double v = f64_mulmod(f64_from_u52(xv[i]) - f64_from_u52(c), di, di * qinv, qd) +
+                       f64_mulmod(f64_from_u52(dv[i]), fd, fd * qinv, qd);
+      o[e] = f64_canon(v, qd, qinv);
+    } else {
+      const uint64_t v = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
+      o[e] = add_mod(v, mul_shoup(dv[i], f, fp, q), q);
+    }
   }
 }
 
