@@ -798,17 +798,27 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
   const size_t n = G.n;
   const size_t d01_stride = 2 * lvl * n, d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n,
                acc_stride = 2 * nm * n;
-  Ws d01(count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
-  if (k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED")) {
+  const bool fused = k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED");
+  // fused path: d0/d1 are formed by their consumers from a and b (no tensor
+  // buffer) unless GPQHE_TENSOR asks for the materialized one (A/B switch)
+  // (and only when out does not overlap an input: ModDown writes out while
+  // other blocks still read a and b)
+  const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
+  const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
+  auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
+  // (the opt-in row form writes d0/d1 from its tensor kernel: buffer needed)
+  const bool lazy = fused && !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) && !overlap(b);
+  Ws d01(lazy ? 0 : count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
+  if (fused) {
     Ws y(count * d2_stride);
     const int mode = rescale ? 1 : 0;
     const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
     const unsigned keep = rescale ? lvl - 1 : lvl;
-    k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride,
-                          (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, dn_fused ? keep : 0,
-                          dn_fused ? keep : nm);
+    const D01Src src = k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride,
+                                             (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl,
+                                             dn_fused ? keep : 0, dn_fused ? keep : nm, lazy);
     if (dn_fused) {
-      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, d01.p, lvl * n);
+      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, src);
       return;
     }
   } else {
@@ -837,9 +847,14 @@ static void mul_chunk_fused(const LaneWs &w, uint64_t *out, size_t out_pstride, 
 {
   const unsigned nm = lvl + G.K, keep = rescale ? lvl - 1 : lvl;
   const size_t n = G.n;
-  k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride,
-                        (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, keep, keep);
-  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, w.d01, lvl * n, w.conv);
+  const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
+  const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
+  auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
+  const D01Src src = k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride,
+                                           (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, keep, keep,
+                                           !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) &&
+                                               !overlap(b));
+  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, src, w.conv);
 }
 
 static void mul_core(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk, bool rescale)

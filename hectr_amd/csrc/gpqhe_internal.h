@@ -279,19 +279,34 @@ void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t see
 void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 bool k_ks_fused_ok();
+// Where the tensor terms d0 = a0 b0 (poly 2 i) and d1 = a0 b1 + a1 b0 (poly
+// 2 i + 1) of ciphertext pair i come from: a materialized buffer (d01 poly P
+// at d01 + P * pstride), or -- d01 == nullptr -- the input pairs themselves
+// (a, b: pair i at + i * in_stride, c1 at + in_pstride), the products formed
+// by each consumer as it reads them.  Limb t word k of a poly sits at
+// (t << logn) + k in both.
+struct D01Src {
+  const uint64_t *d01;
+  size_t pstride;
+  const uint64_t *a, *b;
+  size_t in_stride, in_pstride;
+};
 // Tensor product of `count` pairs (a, b: pair i at + i*in_stride, c1 at +
 // in_pstride) + fused relinearization.  p_lo: P (d0, d1) is added to acc
 // limbs t in [p_lo, lvl) only; the fused ModDown adds the remaining d0/d1
 // terms after its division.  Limbs t >= drop_lo leave after the inverse row
-// pass (input of k_moddown_fused).
-void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
-                           const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
-                           const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo);
+// pass (input of k_moddown_fused).  lazy: d0/d1 are never materialized (d01
+// unused; d2 comes from a fused product + inverse row pass); returns the
+// D01Src that k_moddown_fused must read.
+D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
+                             const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
+                             const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
+                             bool lazy);
 // ModDown (mode 0 or 1) of X fused with the d0/d1 terms left out by
 // k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
-// must hold the inverse row pass of their NTT form; d01 poly p at d01 + p*d01_pstride
+// must hold the inverse row pass of their NTT form
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode, const uint64_t *d01, size_t d01_pstride, uint64_t *conv_ws = nullptr);
+                     unsigned lvl, int mode, const D01Src &d01, uint64_t *conv_ws = nullptr);
 bool k_prof_on();
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();

@@ -41,7 +41,7 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
   KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
-  KC_DN_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
+  KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
   KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
@@ -50,7 +50,7 @@ static const char *kc_names[KC_COUNT] = {
   "ntt_whole_kernel<fwd>", "ntt_whole_kernel<inv>", "ntt_cols_kernel<fwd>", "ntt_rows_kernel<fwd>",
   "ntt_rows_kernel<inv>", "ntt_cols_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
-  "dn_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
+  "dn_rows_kernel", "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel",
   "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>", "gemv_inner_kernel"};
 
@@ -1032,6 +1032,33 @@ __device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, 
   }
 }
 
+// Inverse row pass of one tile whose words the thread already holds in the
+// wave-local coalesced order (raw[i] = word wl_elem(i)).
+template <int LOGN2, bool INV, class A>
+__device__ __forceinline__ void rows8_tile_raw(const A &ar, const uint64_t (&raw)[8], uint64_t *y, uint64_t *lds,
+                                               uint64_t rowbase0)
+{
+  static_assert(INV, "forward tiles load their own words");
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int th = threadIdx.x, row = th / T::TA, h = th % T::TA, l = th % T::TA;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = wl_elem(i);
+    lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = raw[i];
+  }
+  wave_sync();
+  V r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = A::load(lds[T::at(row, 8 * h + k)]);
+  wave_sync();
+  rows8_inv<LOGN2>(r, lds, ar, rowbase0);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+}
+
 template <int LOGN2, bool INV, class A>
 __device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint64_t *y, uint64_t *lds,
                                            uint64_t rowbase0)
@@ -1404,6 +1431,51 @@ void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t ps)
   hipLaunchKernelGGL(neg_kernel, dim3((G.n + TPB - 1) / TPB, lvl, npoly), dim3(TPB), 0, G.stream, x, G.logn, ps,
                      G.dev.mc);
   HIP_CHECK(hipGetLastError());
+}
+
+// Canonical product a b mod q of canonical residues (FP64 for q < 2^51).
+__device__ __forceinline__ uint64_t mulmod_vv(uint64_t a, uint64_t b, const ModConst &m)
+{
+  if (m.q < F64_QMAX) {
+    const double q = (double)m.q, qinv = 1.0 / q, y = f64_from_u52(b);
+    return f64_canon(f64_mulmod(f64_from_u52(a), y, y * qinv, q), q, qinv);
+  }
+  return mul_mod(a, b, m);
+}
+
+// Eight words of tensor poly P (d0 for even P, d1 for odd) at off + pos[k]
+// (off: limb/tile offset inside the poly), canonical mod m.q.
+__device__ __forceinline__ void d01_fetch8(const D01Src &s, unsigned P, size_t off, const int (&pos)[8],
+                                           const ModConst &m, uint64_t (&v)[8])
+{
+  if (s.d01) {
+    const uint64_t *d = s.d01 + P * s.pstride + off;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      v[k] = d[pos[k]];
+    return;
+  }
+  const uint64_t *pa = s.a + (P >> 1) * s.in_stride + off, *pb = s.b + (P >> 1) * s.in_stride + off;
+  if (!(P & 1)) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      v[k] = mulmod_vv(pa[pos[k]], pb[pos[k]], m);
+    return;
+  }
+  if (m.q < F64_QMAX) {
+    const double q = (double)m.q, qinv = 1.0 / q;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const double a0 = f64_from_u52(pa[pos[k]]), a1 = f64_from_u52(pa[s.in_pstride + pos[k]]);
+      const double b0 = f64_from_u52(pb[pos[k]]), b1 = f64_from_u52(pb[s.in_pstride + pos[k]]);
+      v[k] = f64_canon(f64_mulmod(a0, b1, b1 * qinv, q) + f64_mulmod(a1, b0, b0 * qinv, q), q, qinv);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      v[k] = add_mod(mul_mod(pa[pos[k]], pb[s.in_pstride + pos[k]], m),
+                     mul_mod(pa[s.in_pstride + pos[k]], pb[pos[k]], m), m.q);
+  }
 }
 
 // Tensor of count ciphertext pairs: d0 = a0 b0, d1 = a0 b1 + a1 b0 into
@@ -2380,7 +2452,7 @@ __device__ __forceinline__ unsigned own_perm(unsigned idx)
 // t >= drop_lo leave after the inverse row pass (input of dn_cols).
 template <int LOGN2>
 __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
-                                                       size_t d2_stride, const uint64_t *d01, size_t d01_stride,
+                                                       size_t d2_stride, D01Src d01,
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                        unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
@@ -2503,13 +2575,17 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
       (void)f1;
     }
     if (t < lvl && t >= p_lo) {
+      // round C ownership: words 8 h + k of the thread's row
+      int pos[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        pos[k] = (row << LOGN2) + 8 * h + k;
       uint64_t c[8];
-      const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
-      load_own(c0, c);
+      d01_fetch8(d01, 2 * p, ((size_t)t << logn) + toff, pos, mc, c);
 #pragma unroll
       for (int k = 0; k < 8; k++)
         a0[k] = add_mod(a0[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
-      load_own(c0 + ((size_t)lvl << logn), c);
+      d01_fetch8(d01, 2 * p + 1, ((size_t)t << logn) + toff, pos, mc, c);
 #pragma unroll
       for (int k = 0; k < 8; k++)
         a1[k] = add_mod(a1[k], mul_shoup(c[k], mc.pmod, mc.pmodp, q), q);
@@ -2547,7 +2623,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
 // latency is exposed per block instead of several per ciphertext.
 template <int LOGN2>
 __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
-                                                           size_t d2_stride, const uint64_t *d01, size_t d01_stride,
+                                                           size_t d2_stride, D01Src d01,
                                                            const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                            unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                            unsigned nmod, unsigned alpha, unsigned count,
@@ -2685,21 +2761,22 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         (void)f1;
       }
       if (t < lvl && t >= p_lo) {
-        const uint64_t *c0 = d01 + p * d01_stride + ((size_t)t << logn) + toff;
+        // round C ownership is natural order: words 8 th .. 8 th + 7
+        int pos[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          pos[k] = 8 * th + k;
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          const ulonglong2 *v2 = (const ulonglong2 *)(c0 + ((size_t)half * lvl << logn) + 8 * th);
+          uint64_t c[8];
+          d01_fetch8(d01, 2 * p + half, ((size_t)t << logn) + toff, pos, mc, c);
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const ulonglong2 w = v2[i];
-            const uint64_t cl = mul_shoup(w.x, mc.pmod, mc.pmodp, q), ch = mul_shoup(w.y, mc.pmod, mc.pmodp, q);
-            if (half) {
-              a1[2 * i] = add_mod(a1[2 * i], cl, q);
-              a1[2 * i + 1] = add_mod(a1[2 * i + 1], ch, q);
-            } else {
-              a0[2 * i] = add_mod(a0[2 * i], cl, q);
-              a0[2 * i + 1] = add_mod(a0[2 * i + 1], ch, q);
-            }
+          for (int k = 0; k < 8; k++) {
+            const uint64_t cv = mul_shoup(c[k], mc.pmod, mc.pmodp, q);
+            if (half)
+              a1[k] = add_mod(a1[k], cv, q);
+            else
+              a0[k] = add_mod(a0[k], cv, q);
           }
         }
       }
@@ -2739,14 +2816,14 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 
 
 template <int LOGT1, int LOGN2>
-static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const uint64_t *d01,
+static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
                             const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
                             unsigned drop_lo, bool rowform)
 {
   UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
   const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
-               d01_stride = 2 * (size_t)lvl * n, acc_stride = 2 * (size_t)nm * n;
+               acc_stride = 2 * (size_t)nm * n;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned tiles = n / 4096;
   const double own = (double)G.alpha * ndig;  // digit slots not converted (approx. for partial digits)
@@ -2792,12 +2869,12 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     const unsigned members = std::max(1u, std::min(count, want ? want : (6 * 256 + groups - 1) / groups));
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
-                       t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
+                       t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
                        G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc,
                        g_ablate);
   } else {
     hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
-                       T1, t1_stride, d2n, d2_stride, d01, d01_stride, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
+                       T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
                        G.nmod, ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
   }
   HIP_CHECK(hipGetLastError());
@@ -2815,29 +2892,100 @@ static void tensor_rows_launch(uint64_t *d01, uint64_t *d2r, const uint64_t *a, 
   HIP_CHECK(hipGetLastError());
 }
 
+// d2 = a1 b1 of `count` pairs fused with the INTT's inverse row pass: block
+// = (limb, pair, 2048-element row tile), limb-major (one modulus' twiddles
+// hot at a time).  Writes the NTT-form d2 (the own-digit limbs of ks_rows2)
+// and its inverse row pass (the column pass completes the INTT); replaces the
+// tensor kernel and the separate row pass (d0, d1 are formed by their
+// consumers, D01Src).
+template <int LOGN2>
+__global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y, const uint64_t *a,
+                                                       const uint64_t *b, size_t in_stride, size_t in_pstride,
+                                                       unsigned logn, unsigned lvl, unsigned count, Tw2 tw,
+                                                       const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  const unsigned n1 = 1u << (logn - LOGN2), tiles = n1 / T::R;
+  const unsigned blk = blockIdx.x, limb = blk / (count * tiles), rem = blk - limb * count * tiles;
+  const unsigned p = rem / tiles, tile = rem - p * tiles;
+  const ModConst mc = mcs[limb];
+  const unsigned row0 = tile * T::R;
+  const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
+  const uint64_t *pa = a + p * in_stride + in_pstride + off, *pb = b + p * in_stride + in_pstride + off;
+  uint64_t *dn = d2 + (size_t)p * lvl * ((size_t)1 << logn) + off;
+  uint64_t raw[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int e = wl_elem(i);
+    raw[i] = mulmod_vv(pa[e], pb[e], mc);
+    dn[e] = raw[i];
+  }
+  uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
+  with_arith(mc.q, limb, logn, tw, [&](const auto &ar) { rows8_tile_raw<LOGN2, true>(ar, raw, yo, lds, n1 + row0); });
+}
+
 bool k_ks_fused_ok()
 {
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
 }
 
 // Tensor product + fused relinearization core for `count` ciphertext pairs:
-// writes d01 [count][2][lvl] and acc [count][2][nm]; d2 [count][lvl], ybuf and
-// T1 are workspaces.
-void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
-                           const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
-                           const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo)
+// acc [count][2][nm]; d2 [count][lvl], ybuf and T1 are workspaces, d01
+// [count][2][lvl] too unless lazy (then d0/d1 come from a and b, D01Src).
+template <int LOGT1, int LOGN2>
+static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, const uint64_t *b, size_t in_stride,
+                           size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab)
+{
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  const unsigned n = G.n;
+  {
+    // reads a1, b1; writes d2 and its inverse row pass
+    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * 4);
+    hipLaunchKernelGGL((d2_rows_kernel<LOGN2>), dim3(lvl * count * (n / 2048)), dim3(256), 0, G.stream, d2, ybuf, a,
+                       b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc);
+  }
+  LimbSet ys{};
+  ys.base = ybuf;
+  ys.stride = (size_t)lvl * n;
+  ys.per = lvl;
+  ys.count = lvl * count;
+  for (unsigned i = 0; i < lvl; i++)
+    ys.mods[i] = (uint8_t)i;
+  ProfScope ps(KC_NTT2_COLS_INV, 16.0 * n * ys.count);
+  hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(ys.count * (n / 4096)), dim3(256), 0, G.stream, ys, ys,
+                     G.logn, tw, G.dev.mc, (const uint64_t *)tab.ysc);
+  HIP_CHECK(hipGetLastError());
+}
+
+D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
+                             const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
+                             const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
+                             bool lazy)
 {
   UpTable &tab = up_table(lvl);
   // Row form removes the d2 INTT but lengthens the (latency-bound) tensor,
   // ks_cols and ks_rows kernels by more than it saves (20.1k vs 20.7k op/s at
   // N=2^16, L=8); opt-in until those kernels are pipelined.
   const bool rowform = G.alpha <= 4 && G.logn <= 16 && getenv("GPQHE_KS_ROWFORM");
+  if (rowform && lazy)
+    gpqhe_die("k_mul_keyswitch_fused: the row form needs the d01 buffer (lazy = false)");
+  D01Src src{lazy ? nullptr : d01, (size_t)lvl * G.n, a, b, in_stride, in_pstride};
   if (rowform) {
     // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
     if (ks_logn2() == 8)
       tensor_rows_launch<8>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
     else
       tensor_rows_launch<7>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
+  } else if (lazy) {
+    switch (G.logn) {
+    case 13: d2_intt_launch<6, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    case 14: d2_intt_launch<7, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    case 15: d2_intt_launch<7, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    case 16: d2_intt_launch<8, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    case 17: d2_intt_launch<8, 9>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
+    }
   } else {
     k_tensor(d01, d2, a, b, lvl, in_stride, in_pstride, count, (size_t)2 * lvl * G.n);
     LimbSet in{}, out{};
@@ -2852,13 +3000,14 @@ void k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t 
   }
   const uint64_t *y = rowform ? d2 : ybuf;
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 14: ks_fused_launch<7, 7>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 15: ks_fused_launch<7, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 16: ks_fused_launch<8, 8>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 17: ks_fused_launch<8, 9>(y, T1, d2, d01, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
   }
+  return src;
 }
 
 // Montgomery-form copy of a key (x 2^64 mod q per limb), used by the fused
@@ -3243,8 +3392,8 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 // start so their latency overlaps the row pass.
 template <int LOGN2>
 __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint64_t *out, size_t out_pstride,
-                                                       const uint64_t *X, size_t x_pstride, const uint64_t *d01,
-                                                       size_t d01_pstride, unsigned logn, unsigned lvl, unsigned L,
+                                                       const uint64_t *X, size_t x_pstride, D01Src d01,
+                                                       unsigned logn, unsigned lvl, unsigned L,
                                                        unsigned npoly, DownTable tab, Tw2 tw, const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
@@ -3263,14 +3412,15 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   const size_t toff = ((size_t)t << logn) + ((size_t)row0 << LOGN2);
   const uint64_t *x = conv + (((size_t)p * keep) << logn) + toff;
   const uint64_t *xs = X + p * x_pstride + toff;
-  const uint64_t *ds = d01 + p * d01_pstride + toff;
   const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
   uint64_t xv[8], dv[8];
+  int pos[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    xv[i] = xs[wl_elem(i)];
-    dv[i] = ds[wl_elem(i)];
+    pos[i] = wl_elem(i);
+    xv[i] = xs[pos[i]];
   }
+  d01_fetch8(d01, p, toff, pos, mc, dv);
   uint64_t cv[8];
   with_arith(q, m, logn, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
@@ -3306,7 +3456,7 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
 
 template <int LOGT1, int LOGN2>
 static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                            const uint64_t *d01, size_t d01_pstride, unsigned npoly, unsigned lvl, DownTable &tab)
+                            const D01Src &d01, unsigned npoly, unsigned lvl, DownTable &tab)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
@@ -3334,15 +3484,16 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
     else
       go2(std::integral_constant<unsigned, NT>{});
   }
-  // reads conv, X and d01 keep limbs, writes out
-  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 4.0);
+  // reads conv, X and the d0/d1 source (one limb, or lazily the products'
+  // factors: a0 b0 for d0, a0 a1 b0 b1 for d1), writes out
+  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * (d01.d01 ? 4.0 : 6.0));
   hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
-                     out, out_pstride, X, x_pstride, d01, d01_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
+                     out, out_pstride, X, x_pstride, d01, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode, const uint64_t *d01, size_t d01_pstride, uint64_t *conv_ws)
+                     int mode, const D01Src &d01, uint64_t *conv_ws)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
@@ -3351,11 +3502,11 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
   uint64_t *conv = conv_ws ? conv_ws : (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
-  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
-  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
-  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
-  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
-  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, d01_pstride, npoly, lvl, tab); break;
+  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
+  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
+  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
+  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
+  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
   if (!conv_ws)

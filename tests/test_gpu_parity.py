@@ -119,13 +119,18 @@ def test_evaluation_ops(oracle, product, name):
         c = e.ct(); e.mul(c, a, b, rlk); out["mul"] = c
         c = e.ct(); e.mul_rescale(c, a, b, rlk); out["mul_rescale"] = c
         c = e.ct(); e.mul(c, a, b, rlk); e.rescale(c); out["mul_then_rescale"] = c
+        # in place (out aliases an operand): the fused path must not form d0/d1
+        # from inputs it is overwriting
+        c = e.ct(); e.copy_ct(c, a); e.mul_rescale(c, c, b, rlk); out["mul_rescale_inplace"] = c
+        c = e.ct(); e.copy_ct(c, b); e.mul(c, a, c, rlk); out["mul_inplace"] = c
         res[e.name] = (out, sk)
     for op in res["oracle"][0]:
         same(oracle, product, res["oracle"][0][op], res["product"][0][op])
     # decoded sanity on the product side
     out, sk = res["product"]
     expect = {"add": z1 + z2, "sub": z1 - z2, "neg": -z1, "moddown": z1, "rot3": np.roll(z1, -3),
-              "gemv": M @ z1, "mul": z1 * z2, "mul_rescale": z1 * z2, "mul_then_rescale": z1 * z2}
+              "gemv": M @ z1, "mul": z1 * z2, "mul_rescale": z1 * z2, "mul_then_rescale": z1 * z2,
+              "mul_rescale_inplace": z1 * z2, "mul_inplace": z1 * z2}
     for op, want in expect.items():
         got = product.decrypt(out[op], sk)
         assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
@@ -157,19 +162,23 @@ def test_ntt_batch_bitexact(oracle, product, name):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51", "c5",
-                                  "c17"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51",
+                                  "bench51_tensor", "c5", "c17"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
     latter also through the opt-in row-form key switch and through the
-    two-stream chunk pipeline: 5 pairs in chunks of 2) and the config 5 op at
-    n=2^17, L=12 on random-residue ciphertext pairs."""
+    two-stream chunk pipeline: 5 pairs in chunks of 2, and with d0/d1
+    materialized by the tensor kernel instead of formed by their consumers)
+    and the config 5 op at n=2^17, L=12 on random-residue ciphertext pairs."""
     import ctypes
     import torch
     cnt = 3
     if name.endswith("_rowform"):
         monkeypatch.setenv("GPQHE_KS_ROWFORM", "1")
         name = name[:-len("_rowform")]
+    if name.endswith("_tensor"):
+        monkeypatch.setenv("GPQHE_TENSOR", "1")  # materialized d0/d1 (A/B path)
+        name = name[:-len("_tensor")]
     if name.endswith("_lanes"):
         monkeypatch.setenv("GPQHE_CHUNK", "2")
         monkeypatch.setenv("GPQHE_LANES", "1")
