@@ -608,13 +608,28 @@ extern "C" void he_genrlk(he_evk_t *rlk, const poly_mpi_t *sk)
 // Encoding / encryption
 // ===========================================================================
 // Encode z at `scale` into `dst` limbs for moduli mods[0..nm) (NTT domain).
+// Slot counts from which the special FFT runs on the GPU (GPQHE_GPU_ECD_MIN;
+// below it the host FFT plus one upload has the lower latency, e.g. HECTR's
+// 16-32 slots).
+static unsigned gpu_ecd_min()
+{
+  static const unsigned m = env_u("GPQHE_GPU_ECD_MIN", 2048);
+  return m;
+}
+
 static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scale, const unsigned *mods,
                          unsigned nm)
 {
-  std::vector<int64_t> coef(G.n);
-  hm_encode_coeffs(coef.data(), z, s, G.n, scale);
   Ws dcoef(G.n);
-  upload(dcoef.p, coef.data(), (size_t)G.n * 8);
+  if (s >= gpu_ecd_min()) {
+    Ws work(2 * (size_t)s + 2);
+    upload(work.p, z, (size_t)s * 16);
+    k_encode_coeffs((int64_t *)dcoef.p, (double *)work.p, s, scale);
+  } else {
+    std::vector<int64_t> coef(G.n);
+    hm_encode_coeffs(coef.data(), z, s, G.n, scale);
+    upload(dcoef.p, coef.data(), (size_t)G.n * 8);
+  }
   LimbSet ls = limbset(dst, mods, nm, 1, (size_t)nm << G.logn);
   k_lift_ntt(ls, (const int64_t *)dcoef.p);
 }

@@ -222,6 +222,11 @@ uint64_t hm_mul_mod(uint64_t a, uint64_t b, uint64_t q);
 uint64_t hm_pick_prime(unsigned bits, uint64_t two_n, const uint64_t *used, unsigned nused);
 uint64_t hm_find_psi(uint64_t q, uint64_t n);
 unsigned hm_brev(unsigned x, unsigned bits);
+void hm_fft_tables(unsigned s, double *ksi, unsigned *rot);
+// GPU encoder: work (device, 2 s + 2 doubles) holds z (s complex values) and
+// is overwritten; writes the n signed coefficients of hm_encode_coeffs (same
+// operations, same order: bit-identical).  Synchronises (overflow check).
+void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale);
 void hm_encode_coeffs(int64_t *coef, const double *z_interleaved, unsigned s, unsigned n, double scale);
 void hm_decode(double *z_interleaved, const uint64_t *coef_limbs, unsigned nl, unsigned s, unsigned n,
                double scale);

@@ -164,6 +164,19 @@ struct FftTables {
   }
 };
 
+// Tables of the special FFT for s slots, for the GPU encoder: ksi[k] =
+// exp(2 pi i k / 4s) for k <= 4s as (re, im) pairs, rot[j] = 5^j mod 4s.
+void hm_fft_tables(unsigned s, double *ksi, unsigned *rot)
+{
+  FftTables T(s);
+  for (unsigned k = 0; k <= 4 * s; k++) {
+    ksi[2 * k] = T.ksi[k].re;
+    ksi[2 * k + 1] = T.ksi[k].im;
+  }
+  for (unsigned j = 0; j < s; j++)
+    rot[j] = T.rot[j];
+}
+
 static void bitrev_perm(cplx *v, unsigned s)
 {
   const unsigned lb = (unsigned)__builtin_ctz(s);

@@ -1641,6 +1641,134 @@ void k_sample_uniform(const LimbSet &dst, uint64_t stream)
   HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// GPU CKKS encoder (he_ecd for large slot counts): the special inverse FFT of
+// host_math.cpp (fft_special_enc) stage by stage with the same operations in
+// the same order (IEEE products, sums and division, no contraction: this file
+// is built with -ffp-contract=off), then bit reversal, / s, x scale and
+// llround.  Bit-identical to the host encoder and the oracle.
+//   stages with len > FFT_LDS: one launch each, a thread per butterfly;
+//   stages with len <= FFT_LDS: one launch, a block per FFT_LDS-element chunk
+//   in LDS (the chunks are independent below that length).
+// ---------------------------------------------------------------------------
+constexpr unsigned FFT_LDS = 2048;
+
+__device__ __forceinline__ void fft_enc_bfly(double2 &x, double2 &y, const double2 w)
+{
+  const double2 a = make_double2(x.x + y.x, x.y + y.y);
+  const double2 d = make_double2(x.x - y.x, x.y - y.y);
+  x = a;
+  y = make_double2(d.x * w.x - d.y * w.y, d.x * w.y + d.y * w.x);
+}
+
+__global__ void fft_enc_stage_kernel(double2 *v, unsigned s, unsigned len, const double2 *ksi, const unsigned *rot)
+{
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= s / 2)
+    return;
+  const unsigned h = len >> 1, lq = len << 2, M = 4 * s;
+  const unsigned i = (t / h) * len, j = t % h;
+  const unsigned idx = (lq - rot[j] % lq) * (M / lq);
+  fft_enc_bfly(v[i + j], v[i + j + h], ksi[idx]);
+}
+
+__global__ void __launch_bounds__(512) fft_enc_lds_kernel(double2 *v, unsigned s, unsigned len0, const double2 *ksi,
+                                                          const unsigned *rot)
+{
+  __shared__ double2 c[FFT_LDS];
+  const unsigned base = blockIdx.x * len0, M = 4 * s;
+  for (unsigned e = threadIdx.x; e < len0; e += blockDim.x)
+    c[e] = v[base + e];
+  __syncthreads();
+  for (unsigned len = len0; len >= 2; len >>= 1) {
+    const unsigned h = len >> 1, lq = len << 2;
+    for (unsigned t = threadIdx.x; t < len0 / 2; t += blockDim.x) {
+      const unsigned i = (t / h) * len, j = t % h;
+      const unsigned idx = (lq - rot[j] % lq) * (M / lq);
+      fft_enc_bfly(c[i + j], c[i + j + h], ksi[idx]);
+    }
+    __syncthreads();
+  }
+  for (unsigned e = threadIdx.x; e < len0; e += blockDim.x)
+    v[base + e] = c[e];
+}
+
+// coef[k gap] = llround(re(u_k) / s * scale), coef[(k + s) gap] = im, 0
+// elsewhere; u = bit-reversed v.  One thread per coefficient slot pair.
+__global__ void fft_enc_round_kernel(int64_t *coef, const double2 *v, unsigned s, unsigned logs, unsigned n,
+                                     double scale, int *overflow)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n / 2)
+    return;
+  const unsigned gap = n / (2 * s);
+  int64_t lo = 0, hi = 0;
+  if (k % gap == 0) {
+    const unsigned slot = k / gap;
+    const double2 u = v[logs ? __brev(slot) >> (32 - logs) : 0];
+    const double re = u.x / (double)s * scale, im = u.y / (double)s * scale;
+    if (fabs(re) >= 9.2e18 || fabs(im) >= 9.2e18)
+      *overflow = 1;
+    lo = llround(re);
+    hi = llround(im);
+  }
+  coef[k] = lo;
+  coef[k + n / 2] = hi;
+}
+
+struct FftDev {
+  double2 *ksi;
+  unsigned *rot;
+};
+static std::map<unsigned, FftDev> g_fft;
+
+void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale)
+{
+  const unsigned n = G.n;
+  if (!s || (s & (s - 1)) || s > n / 2)
+    gpqhe_die("bad slot count %u", s);
+  auto it = g_fft.find(s);
+  if (it == g_fft.end()) {
+    std::vector<double> ksi(2 * (4 * (size_t)s + 1));
+    std::vector<unsigned> rot(s);
+    hm_fft_tables(s, ksi.data(), rot.data());
+    FftDev d;
+    HIP_CHECK(hipMalloc(&d.ksi, ksi.size() * 8));
+    HIP_CHECK(hipMalloc(&d.rot, rot.size() * 4));
+    HIP_CHECK(hipMemcpy(d.ksi, ksi.data(), ksi.size() * 8, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d.rot, rot.data(), rot.size() * 4, hipMemcpyHostToDevice));
+    it = g_fft.emplace(s, d).first;
+  }
+  const FftDev &T = it->second;
+  double2 *v = (double2 *)work;
+  unsigned len = s;
+  for (; len > FFT_LDS; len >>= 1)
+    hipLaunchKernelGGL(fft_enc_stage_kernel, dim3((s / 2 + TPB - 1) / TPB), dim3(TPB), 0, G.stream, v, s, len, T.ksi,
+                       T.rot);
+  if (len >= 2)
+    hipLaunchKernelGGL(fft_enc_lds_kernel, dim3(s / len), dim3(std::min(512u, std::max(64u, len / 2))), 0, G.stream,
+                       v, s, len, T.ksi, T.rot);
+  int *ovf = (int *)(work + 2 * (size_t)s);
+  HIP_CHECK(hipMemsetAsync(ovf, 0, sizeof(int), G.stream));
+  hipLaunchKernelGGL(fft_enc_round_kernel, dim3((n / 2 + TPB - 1) / TPB), dim3(TPB), 0, G.stream, coef, v, s,
+                     (unsigned)__builtin_ctz(s), n, scale, ovf);
+  HIP_CHECK(hipGetLastError());
+  int h = 0;
+  HIP_CHECK(hipMemcpyAsync(&h, ovf, sizeof(int), hipMemcpyDeviceToHost, G.stream));
+  HIP_CHECK(hipStreamSynchronize(G.stream));
+  if (h)
+    gpqhe_die("encode overflow (|value * scale| >= 2^63)");
+}
+
+void k_fft_free()
+{
+  for (auto &kv : g_fft) {
+    HIP_CHECK(hipFree(kv.second.ksi));
+    HIP_CHECK(hipFree(kv.second.rot));
+  }
+  g_fft.clear();
+}
+
 __global__ void lift_i64_kernel(LimbSet dst, const int64_t *coef, unsigned logn, const ModConst *mc)
 {
   const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3638,4 +3766,5 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.cd));
   }
   g_down.clear();
+  k_fft_free();
 }

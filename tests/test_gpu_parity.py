@@ -285,3 +285,32 @@ def test_gemv_zero_matrix(oracle, product):
     e, y, sk = res["product"]
     assert np.abs(e.decrypt(y, sk)).max() < 1e-6
 
+
+
+@pytest.mark.parametrize("name,slots", [("c1", 2048), ("c1", 4096), ("bench51", 32768), ("bench51", 4096)])
+def test_gpu_encode_bitexact(oracle, product, name, slots):
+    """he_ecd with the special FFT on the GPU (slot counts
+    >= GPQHE_GPU_ECD_MIN = 2048): the LDS-only transform (2048 slots) and the
+    global + LDS stages (4096 and the full n/2 = 32768 slots at n=2^16) give
+    the host/oracle encoding bit for bit, and it decrypts to the input."""
+    init_both(oracle, product, name)
+    rng = np.random.default_rng(slots)
+    z = rng.uniform(-1, 1, slots) + 1j * rng.uniform(-1, 1, slots)
+    delta = product.info.delta
+    res = {}
+    for e in (oracle, product):
+        pt = e.pt()
+        e.ecd_ex(pt, z, slots, delta, e.L)
+        res[e.name] = e.export(pt)
+        e.free(pt)
+    assert np.array_equal(res["oracle"], res["product"]), \
+        f"{np.count_nonzero(res['oracle'] != res['product'])} residues differ"
+    pk, sk, _, _ = keys(product, rot=False)
+    pt, ct, dec = product.pt(), product.ct(), product.pt()
+    product.ecd_ex(pt, z, slots, delta, product.L)
+    product.enc_pk(ct, pt, pk)
+    product.dec(dec, ct, sk)
+    got = product.dcd(dec, slots)
+    assert np.abs(got - z).max() < 1e-6
+    for o in (pt, ct, dec):
+        product.free(o)
