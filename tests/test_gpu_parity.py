@@ -15,6 +15,8 @@ Parameter sets:
           key inner product run on the FP64 path
   c17   : n=2^17, L=8, K=4, dnum=2, primes < 2^51 (the 2^17 fused path with the
           key-stationary two-digit inner product)
+  c14/c15: n=2^14 (all primes < 2^51) and n=2^15 (60-bit q0/P: mixed FP64 and
+          integer limbs), L=6, K=3, dnum=2 -- the other fused tilings
 Integer results must match exactly; decoded values are compared with the
 closed-loop tolerance of the CSTR test (1e-6 relative, reference achieves
 1e-11).
@@ -36,6 +38,10 @@ PARAMS = {
     "bench51": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50,
                                p_bits=51)),
     "c17": ("params", dict(logn=17, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50, p_bits=51)),
+    # the remaining fused-path tilings: n=2^14 (64 x 256 columns, 128-element
+    # rows) and n=2^15 (128 x 256 columns, 256-element rows)
+    "c14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
+    "c15": ("params", dict(logn=15, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=60, qi_bits=48, p_bits=60)),
 }
 
 
@@ -136,7 +142,7 @@ def test_evaluation_ops(oracle, product, name):
         assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
 
 
-@pytest.mark.parametrize("name", ["bench", "bench51", "c5"])
+@pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c14", "c15"])
 def test_ntt_batch_bitexact(oracle, product, name):
     """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain on a
     4-polynomial sample: forward, then inverse (the roundtrip identity)."""
@@ -163,7 +169,7 @@ def test_ntt_batch_bitexact(oracle, product, name):
 
 
 @pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51",
-                                  "bench51_tensor", "c5", "c17"])
+                                  "bench51_tensor", "c5", "c17", "c14", "c15"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
     latter also through the opt-in row-form key switch and through the
