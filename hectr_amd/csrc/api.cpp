@@ -1076,13 +1076,20 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
   const size_t per_ct = (size_t)(2 * lvl + 2 * lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
-  const size_t budget = (size_t)2 << 30;
+  // workspace per chunk (GPQHE_WS_MIB, default 4 GiB: 86 pairs at N=2^16, L=8,
+  // dnum=2).  Bigger chunks fill the GPU better (dn_cols has 32 blocks per
+  // pair) and amortize ks_rows2's key tiles over longer runs: same-box A/B
+  // 27.3k (2 GiB) vs 28.3-28.6k (2.5-4 GiB); 288 GB of HBM leave room.
+  static const size_t budget = (size_t)env_u("GPQHE_WS_MIB", 4096) << 20;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));
   if (const char *e = getenv("GPQHE_CHUNK"))  // test hook: force small chunks (several lanes' worth)
     chunk = std::max<size_t>(1, std::min<size_t>(chunk, strtoul(e, nullptr, 0)));
-  const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
+  // equal chunks: a short last chunk runs at a fraction of the GPU's width
   const size_t nchunks = (count + chunk - 1) / chunk;
+  if (nchunks)
+    chunk = (count + nchunks - 1) / nchunks;
+  const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
   const bool lanes = nchunks >= 2 && k_ks_fused_ok() && rlk->reserved && rlk->dnum == G.dnum &&
                      !getenv("GPQHE_UNFUSED") && !getenv("GPQHE_DN_UNFUSED") && getenv("GPQHE_LANES") &&
                      !k_prof_on();
