@@ -829,11 +829,15 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
     const int mode = rescale ? 1 : 0;
     const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
     const unsigned keep = rescale ? lvl - 1 : lvl;
-    const D01Src src = k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride,
-                                             (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl,
-                                             dn_fused ? keep : 0, dn_fused ? keep : nm, lazy);
+    // keep slots' MAC deferred into the ModDown rows (kd_rows_kernel)
+    const bool defer = dn_fused && k_ks_defer_ok(lvl);
+    const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
+    const D01Src src = k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride, evkm, count,
+                                             lvl, dn_fused ? keep : 0, dn_fused ? keep : nm, lazy,
+                                             defer ? keep : 0);
     if (dn_fused) {
-      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, src);
+      const KsDeferred ks{D.p, d2.p, evkm};
+      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, src, nullptr, defer ? &ks : nullptr);
       return;
     }
   } else {
@@ -865,11 +869,16 @@ static void mul_chunk_fused(const LaneWs &w, uint64_t *out, size_t out_pstride, 
   const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
   const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
   auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
-  const D01Src src = k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride,
-                                           (const uint64_t *)(uintptr_t)rlk->reserved, count, lvl, keep, keep,
+  const bool defer = k_ks_defer_ok(lvl);
+  const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
+  const D01Src src = k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride, evkm, count,
+                                           lvl, keep, keep,
                                            !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) &&
-                                               !overlap(b));
-  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, src, w.conv);
+                                               !overlap(b),
+                                           defer ? keep : 0);
+  const KsDeferred ks{w.T1, w.d2, evkm};
+  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, src, w.conv,
+                  defer ? &ks : nullptr);
 }
 
 static void mul_core(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk, bool rescale)

@@ -302,16 +302,26 @@ struct D01Src {
 // terms after its division.  Limbs t >= drop_lo leave after the inverse row
 // pass (input of k_moddown_fused).  lazy: d0/d1 are never materialized (d01
 // unused; d2 comes from a fused product + inverse row pass); returns the
-// D01Src that k_moddown_fused must read.
+// D01Src that k_moddown_fused must read.  t_lo > 0 (k_ks_defer_ok): acc slots
+// below t_lo are not computed (k_moddown_fused's KsDeferred does them).
 D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
                              const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
                              const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
-                             bool lazy);
+                             bool lazy, unsigned t_lo = 0);
+// Inputs of the key-switch slots that k_mul_keyswitch_fused left to the
+// ModDown (t_lo = keep): T1 and the NTT-form d2 of the same call, the
+// Montgomery-form key.  Strides as k_mul_keyswitch_fused's workspaces.
+struct KsDeferred {
+  const uint64_t *T1, *d2, *evkm;
+};
+bool k_ks_defer_ok(unsigned lvl);
 // ModDown (mode 0 or 1) of X fused with the d0/d1 terms left out by
 // k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
-// must hold the inverse row pass of their NTT form
+// must hold the inverse row pass of their NTT form.  ks != nullptr: X's keep
+// limbs were not computed (t_lo = keep); their MAC runs here from ks.
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode, const D01Src &d01, uint64_t *conv_ws = nullptr);
+                     unsigned lvl, int mode, const D01Src &d01, uint64_t *conv_ws = nullptr,
+                     const KsDeferred *ks = nullptr);
 bool k_prof_on();
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();

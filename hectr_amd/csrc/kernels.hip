@@ -42,7 +42,7 @@ enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
   KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
   KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
-  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_COUNT
+  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KD_ROWS, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
@@ -52,7 +52,7 @@ static const char *kc_names[KC_COUNT] = {
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
   "dn_rows_kernel", "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel",
-  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>", "gemv_inner_kernel"};
+  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>", "gemv_inner_kernel", "kd_rows_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -693,10 +693,11 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
 #pragma unroll
     for (int it = 0; it < C / 16; it++) {
       const int item = t + 256 * it, c = item % C, l = item / C;
+      const unsigned vo = (unsigned)l * n2 + c;  // 32-bit per-thread offset, uniform row bases
       V r[EA];
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        r[k] = A::load(x[(size_t)(l + 16 * k) * n2 + c]);
+        r[k] = A::load((x + (size_t)(16 * k) * n2)[vo]);
       ar.template fwd<LEA>(r, T, LOGT - 1);
 #pragma unroll
       for (int k = 0; k < EA; k++)
@@ -705,6 +706,7 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
     __syncthreads();
     // round B: rows 16 g + k (distances 8 .. 1)
     const int c = t % C, g = t / C;
+    const unsigned vo = (unsigned)(16 * g) * n2 + c;
     V r[16];
 #pragma unroll
     for (int k = 0; k < 16; k++)
@@ -712,14 +714,15 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
     ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
     for (int k = 0; k < 16; k++)
-      y[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+      (y + (size_t)k * n2)[vo] = ar.canon(r[k]);
   } else {
     {
       const int c = t % C, g = t / C;
+      const unsigned vo = (unsigned)(16 * g) * n2 + c;
       V r[16];
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        r[k] = A::load(x[(size_t)(16 * g + k) * n2 + c]);
+        r[k] = A::load((x + (size_t)k * n2)[vo]);
       ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
       for (int k = 0; k < 16; k++)
@@ -729,6 +732,7 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
 #pragma unroll
     for (int it = 0; it < C / 16; it++) {
       const int item = t + 256 * it, c = item % C, l = item / C;
+      const unsigned vo = (unsigned)l * n2 + c;
       V r[EA];
 #pragma unroll
       for (int k = 0; k < EA; k++)
@@ -736,7 +740,7 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
       ar.template inv<LEA>(r, T, 4);
 #pragma unroll
       for (int k = 0; k < EA; k++)
-        y[(size_t)(l + 16 * k) * n2 + c] = ar.mulc(r[k], sw, swp);
+        (y + (size_t)(16 * k) * n2)[vo] = ar.mulc(r[k], sw, swp);
     }
   }
 }
@@ -2432,11 +2436,12 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
 #pragma unroll
     for (int it = 0; it < IT; it++) {
       const int item = th + 256 * it, c = item % C, l = item / C;
+      const unsigned vo = (unsigned)l * n2 + c;  // 32-bit per-thread offset, uniform bases
 #pragma unroll
       for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          const uint64_t v = i < (int)na ? yb[((size_t)i << logn) + (size_t)(l + 16 * k) * n2 + c] : 0;
+          const uint64_t v = i < (int)na ? (yb + ((size_t)i << logn) + (size_t)(16 * k) * n2)[vo] : 0;
           y[it][i][k] = F64 ? (uint64_t)__double_as_longlong(f64_from_u52(v)) : v;
         }
     }
@@ -2463,10 +2468,11 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         using V = typename A::V;
         {
           const int c = th % C, g = th / C;
+          const unsigned vo = (unsigned)(16 * g) * n2 + c;
           V r[16];
 #pragma unroll
           for (int k = 0; k < 16; k++)
-            r[k] = A::load(src[(size_t)(16 * g + k) * n2 + c]);
+            r[k] = A::load((src + (size_t)k * n2)[vo]);
           ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
           for (int k = 0; k < 16; k++)
@@ -2550,6 +2556,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       }
       __syncthreads();
       const int c = th % C, g = th / C;
+      const unsigned vo = (unsigned)(16 * g) * n2 + c;
       V r[16];
 #pragma unroll
       for (int k = 0; k < 16; k++)
@@ -2557,7 +2564,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+        (out + (size_t)k * n2)[vo] = ar.canon(r[k]);
     });
     (void)q2;
   }
@@ -2756,21 +2763,21 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
                                                            unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                            unsigned nmod, unsigned alpha, unsigned count,
                                                            unsigned cpb, unsigned members, unsigned p_lo,
-                                                           unsigned drop_lo, int own_rowform, Tw2 tw,
-                                                           const ModConst *mcs, int ablate)
+                                                           unsigned drop_lo, unsigned t_lo, int own_rowform,
+                                                           Tw2 tw, const ModConst *mcs, int ablate)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
   __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
-  unsigned grp, mi;  // group = (basis slot t, tile) on one XCD; members = ciphertext runs
-  if (!xcd_group(members, nm * tiles, grp, mi))
+  unsigned grp, mi;  // group = (basis slot t >= t_lo, tile) on one XCD; members = ciphertext runs
+  if (!xcd_group(members, (nm - t_lo) * tiles, grp, mi))
     return;
   const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
   if (p0 >= p1)
     return;
-  const unsigned t = grp / tiles, tile = grp % tiles;
+  const unsigned t = t_lo + grp / tiles, tile = grp % tiles;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
   const uint64_t q = mc.q, q2 = 2 * q;
@@ -2946,7 +2953,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
                             const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
-                            unsigned drop_lo, bool rowform)
+                            unsigned drop_lo, unsigned t_lo, bool rowform)
 {
   UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
@@ -2985,21 +2992,26 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
     }
   }
-  // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key once, writes acc
+  // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key
+  // once, writes acc; slots [t_lo, nm) only (t_lo > 0: kd_rows_kernel does the
+  // lower slots inside the ModDown)
   const bool rows2 = ndig == 2 && !getenv("GPQHE_KSROWS_STREAM");
+  if (t_lo && !rows2)
+    gpqhe_die("deferred key-switch slots need the two-digit ks_rows2 path");
+  const double ns = nm - t_lo;
   ProfScope ps(rows2 ? KC_KS_ROWS2 : KC_KS_ROWS,
-               8.0 * n * ((double)count * (ndig * nm - own + lvl + 2.0 * (lvl - std::min(p_lo, lvl)) +
-                                                       2 * nm) + 2.0 * ndig * nm));
+               8.0 * n * ((double)count * (ndig * ns + 2.0 * (lvl - std::min(p_lo, lvl)) + 2 * ns) +
+                          2.0 * ndig * ns));
   if (rows2) {
     // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
-    const unsigned groups = nm * (n / 2048);
+    const unsigned groups = (nm - t_lo) * (n / 2048);
     static const unsigned want = getenv("GPQHE_KSR_MEMBERS") ? atoi(getenv("GPQHE_KSR_MEMBERS")) : 0;
     const unsigned members = std::max(1u, std::min(count, want ? want : (6 * 256 + groups - 1) / groups));
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
                        t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc,
-                       g_ablate);
+                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, t_lo, rowform ? 1 : 0, tw,
+                       G.dev.mc, g_ablate);
   } else {
     hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
                        T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
@@ -3058,6 +3070,20 @@ bool k_ks_fused_ok()
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
 }
 
+// The keep slots' MAC can move into the ModDown rows (kd_rows_kernel) when the
+// key has two digits (ks_rows2's key-stationary layout) and d2 stays in NTT
+// form (no row form).  Opt-in (GPQHE_KDROWS=1): it removes the keep limbs'
+// accumulator round trip (28 of ~235 limb transfers per pair at N=2^16, L=8,
+// dnum=2) but measured no faster (28.7k vs 28.6k ct-mult/s same box: the row
+// kernels are latency-bound, and kd_rows spills at 256 VGPRs).
+bool k_ks_defer_ok(unsigned lvl)
+{
+  // (read per call: the switches are per-call, as the row form's)
+  const char *e = getenv("GPQHE_KDROWS");
+  const bool on = e && atoi(e) && !getenv("GPQHE_KSROWS_STREAM") && !getenv("GPQHE_KS_ROWFORM");
+  return on && k_ks_fused_ok() && (lvl + G.alpha - 1) / G.alpha == 2;
+}
+
 // Tensor product + fused relinearization core for `count` ciphertext pairs:
 // acc [count][2][nm]; d2 [count][lvl], ybuf and T1 are workspaces, d01
 // [count][2][lvl] too unless lazy (then d0/d1 come from a and b, D01Src).
@@ -3089,7 +3115,7 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
 D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
                              const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
                              const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
-                             bool lazy)
+                             bool lazy, unsigned t_lo)
 {
   UpTable &tab = up_table(lvl);
   // Row form removes the d2 INTT but lengthens the (latency-bound) tensor,
@@ -3098,6 +3124,8 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
   const bool rowform = G.alpha <= 4 && G.logn <= 16 && getenv("GPQHE_KS_ROWFORM");
   if (rowform && lazy)
     gpqhe_die("k_mul_keyswitch_fused: the row form needs the d01 buffer (lazy = false)");
+  if (rowform && t_lo)
+    gpqhe_die("k_mul_keyswitch_fused: deferred slots need the NTT-form d2 limbs (no row form)");
   D01Src src{lazy ? nullptr : d01, (size_t)lvl * G.n, a, b, in_stride, in_pstride};
   if (rowform) {
     // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
@@ -3128,11 +3156,11 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
   }
   const uint64_t *y = rowform ? d2 : ybuf;
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
-  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, rowform); break;
+  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
+  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
+  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
+  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
+  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
   }
   return src;
@@ -3398,11 +3426,14 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       using A = std::decay_t<decltype(ar)>;
       using V = typename A::V;
       {
+        // 32-bit per-thread offset + uniform per-row base (scalar address
+        // arithmetic; 64-bit per-element offsets cost 32 VGPRs and spilled)
         const int c = th % C, g = th / C;
+        const unsigned vo = (unsigned)(16 * g) * n2 + c;
         V r[16];
 #pragma unroll
         for (int k = 0; k < 16; k++)
-          r[k] = A::load(src[(size_t)(16 * g + k) * n2 + c]);
+          r[k] = A::load((src + (size_t)k * n2)[vo]);
         ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
         for (int k = 0; k < 16; k++)
@@ -3502,6 +3533,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       }
       __syncthreads();
       const int c = th % C, g = th / C;
+      const unsigned vo = (unsigned)(16 * g) * n2 + c;
       V r[16];
 #pragma unroll
       for (int k = 0; k < 16; k++)
@@ -3509,7 +3541,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        out[(size_t)(16 * g + k) * n2 + c] = ar.canon(r[k]);
+        (out + (size_t)k * n2)[vo] = ar.canon(r[k]);
     });
     (void)q2;
   }
@@ -3582,9 +3614,174 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   }
 }
 
+// Keep slots of the fused relinearization, deferred into the ModDown (the
+// accumulator's keep limbs never reach HBM).  A block owns (keep slot t, row
+// tile) and a run of ciphertexts with the key tile of both digits stationary
+// in LDS, as ks_rows2_kernel: per ciphertext the row pass of the non-own
+// digit's T1 limb and the MAC give X_0, X_1 (round C ownership, natural order)
+// in registers; then, per poly, the forward row pass of conv_t and the
+// dn_rows_kernel epilogue  out = (X - conv) Dprod^-1 + fin_t d01_t.
+// Inputs: T1 / d2 / key as ks_rows2_kernel, conv as dn_rows_kernel.
+template <int LOGN2>
+__global__ void __launch_bounds__(256, 2) kd_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
+                                                          size_t d2_stride, const uint64_t *evkm,
+                                                          const uint64_t *conv, uint64_t *out, size_t out_pstride,
+                                                          D01Src d01, unsigned logn, unsigned lvl, unsigned L,
+                                                          unsigned nm, unsigned nmod, unsigned alpha, unsigned count,
+                                                          unsigned cpb, unsigned members, DownTable tab, Tw2 tw,
+                                                          const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / T::R;
+  const unsigned keep = tab.keep;
+  unsigned grp, mi;  // group = (keep slot t, tile) on one XCD; members = ciphertext runs
+  if (!xcd_group(members, keep * tiles, grp, mi))
+    return;
+  const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
+  if (p0 >= p1)
+    return;
+  const unsigned t = grp / tiles, tile = grp % tiles;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * T::R;
+  const size_t toff = (size_t)row0 << LOGN2, loff = ((size_t)t << logn) + toff;
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
+  const unsigned own = t / alpha;  // t < lvl: digit `own` holds slot t as its NTT-form d2 limb
+  auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
+    if (j == own) {
+      // round C ownership is natural order: thread th holds words 8 th .. 8 th + 7
+      const ulonglong2 *v2 = (const ulonglong2 *)(d2n + p * d2_stride + loff + 8 * th);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const ulonglong2 w = v2[i];
+        x[2 * i] = w.x;
+        x[2 * i + 1] = w.y;
+      }
+    } else {
+      const uint64_t *s_ = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        x[k] = s_[(row << LOGN2) + l + T::TA * k];
+    }
+  };
+  const bool f64 = q < F64_QMAX && tw.fwdd;  // the key tile is plain for these moduli (to_mont_kernel)
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
+      kl[c][256 * k + th] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
+    }
+  uint64_t xn[2][8];
+  fetch(xn[0], 0, p0);
+  fetch(xn[1], 1, p0);
+  auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
+    const uint64_t lo = v * w, hi = mulhi64(v, w);
+    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
+    a = lazy_lt2q(a + r, q2);
+  };
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], fin = tab.fin[2 * t], finp = tab.fin[2 * t + 1];
+  int pos[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    pos[k] = 8 * th + k;
+  with_arith(q, m, logn, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    using V = typename A::V;
+    for (unsigned p = p0; p < p1; p++) {
+      uint64_t a0[8], a1[8];
+      V f0[8], f1[8];  // FP64 accumulators (|.| < 3q: two products of < 1.5q each)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        V r[8];
+        wave_sync();  // the previous phase has finished with the LDS tile
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          r[k] = A::load(xn[j][k]);
+        if (p + 1 < p1)
+          fetch(xn[j], j, p + 1);  // prefetch: in flight during the rest of this ciphertext
+        if (j != (int)own)
+          rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
+        if constexpr (std::is_same<A, ArF64>::value) {
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
+            const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
+            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
+            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
+            f0[k] = j ? f0[k] + tb : tb;
+            f1[k] = j ? f1[k] + ta : ta;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const uint64_t v = ar.canon(r[k]);
+            if (j == 0)
+              a0[k] = a1[k] = 0;
+            mac(a0[k], v, kl[2 * j][256 * k + th]);
+            mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
+          }
+        }
+      }
+      if constexpr (std::is_same<A, ArF64>::value) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          a0[k] = ar.canon(f0[k]);
+          a1[k] = ar.canon(f1[k]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+          a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+        }
+        (void)f0;
+        (void)f1;
+      }
+      // ModDown of both polys: conv_t row pass + epilogue (dn_rows_kernel)
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        const unsigned P = 2 * p + half;
+        const uint64_t *x = conv + (((size_t)P * keep + t) << logn) + toff;
+        V r[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+        uint64_t dv[8], cv[8];
+        d01_fetch8(d01, P, loff, pos, mc, dv);
+        wave_sync();
+        rows8_fwd<LOGN2>(r, cv, lds, ar, n1 + row0);
+        uint64_t o[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint64_t xv = half ? a1[k] : a0[k];
+          if (q < F64_QMAX) {
+            // exact FP64 products: |X - conv| < q, each product < 1.25 q
+            const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv), fd = f64_from_u52(fin);
+            const double v = f64_mulmod(f64_from_u52(xv) - f64_from_u52(cv[k]), di, di * qinv, qd) +
+                             f64_mulmod(f64_from_u52(dv[k]), fd, fd * qinv, qd);
+            o[k] = f64_canon(v, qd, qinv);
+          } else {
+            const uint64_t v = mul_shoup(sub_mod(xv, cv[k], q), dinv, dinvp, q);
+            o[k] = add_mod(v, mul_shoup(dv[k], fin, finp, q), q);
+          }
+        }
+        ulonglong2 *d2o = (ulonglong2 *)(out + P * out_pstride + loff + 8 * th);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          d2o[i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
+      }
+    }
+  });
+}
+
 template <int LOGT1, int LOGN2>
 static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                            const D01Src &d01, unsigned npoly, unsigned lvl, DownTable &tab)
+                            const D01Src &d01, unsigned npoly, unsigned lvl, DownTable &tab, const KsDeferred *ks)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
@@ -3612,6 +3809,20 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
     else
       go2(std::integral_constant<unsigned, NT>{});
   }
+  if (ks) {
+    // keep slots' key-switch MAC here (ks_rows2 ran the drop slots only): reads
+    // per pair and keep slot the two digits' inputs, conv and the d0/d1 source
+    // of both polys, writes both; the key tiles once
+    const unsigned nm = lvl + G.K, count = npoly / 2, groups = keep * (n / 2048);
+    const unsigned members = std::max(1u, std::min(count, (6 * 256 + groups - 1) / groups));
+    const unsigned cpb = (count + members - 1) / members;
+    ProfScope ps(KC_KD_ROWS, 8.0 * n * ((double)count * keep * (2 + 2 + (d01.d01 ? 2.0 : 6.0) + 2) + 4.0 * keep));
+    hipLaunchKernelGGL((kd_rows_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, ks->T1,
+                       (size_t)2 * nm * n, ks->d2, (size_t)lvl * n, ks->evkm, conv, out, out_pstride, d01, G.logn, lvl,
+                       G.L, nm, G.nmod, G.alpha, count, cpb, members, tab, tw, G.dev.mc);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   // reads conv, X and the d0/d1 source (one limb, or lazily the products'
   // factors: a0 b0 for d0, a0 a1 b0 b1 for d1), writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * (d01.d01 ? 4.0 : 6.0));
@@ -3621,7 +3832,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
 }
 
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode, const D01Src &d01, uint64_t *conv_ws)
+                     int mode, const D01Src &d01, uint64_t *conv_ws, const KsDeferred *ks)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
@@ -3630,11 +3841,11 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
   uint64_t *conv = conv_ws ? conv_ws : (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
-  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
-  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
-  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
-  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
-  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab); break;
+  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
+  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
+  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
+  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
+  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
   if (!conv_ws)

@@ -169,16 +169,22 @@ def test_ntt_batch_bitexact(oracle, product, name):
 
 
 @pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51",
-                                  "bench51_tensor", "c5", "c17", "c14", "c15"])
+                                  "bench51_tensor", "c5", "c17", "c14", "c15", "bench_d2_kd", "bench51_kd",
+                                  "bench51_tensor_kd", "c14_kd", "c15_kd", "c17_kd"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
     latter also through the opt-in row-form key switch and through the
     two-stream chunk pipeline: 5 pairs in chunks of 2, and with d0/d1
     materialized by the tensor kernel instead of formed by their consumers)
-    and the config 5 op at n=2^17, L=12 on random-residue ciphertext pairs."""
+    and the config 5 op at n=2^17, L=12 on random-residue ciphertext pairs.
+    "_kd": the opt-in path that moves the keep slots' key-switch MAC into the
+    ModDown rows (GPQHE_KDROWS, kd_rows_kernel)."""
     import ctypes
     import torch
     cnt = 3
+    if name.endswith("_kd"):
+        monkeypatch.setenv("GPQHE_KDROWS", "1")
+        name = name[:-len("_kd")]
     if name.endswith("_rowform"):
         monkeypatch.setenv("GPQHE_KS_ROWFORM", "1")
         name = name[:-len("_rowform")]
