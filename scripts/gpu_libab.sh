@@ -17,5 +17,9 @@ B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr --no-ntt --alt-bits 
 for r in $(seq 1 ${ROUNDS:-2}); do
   GPQHE_LIB=hectr_amd/lib_base/libgpqhe.so timeout -k 10 300 $B > $OUT/bench_base_$r.log 2>&1 || exit 1
   timeout -k 10 300 $B > $OUT/bench_new_$r.log 2>&1 || exit 1
+  # VARIANTS="name=ENVVAR=VALUE ...": the working tree's library under env switches
+  for v in ${VARIANTS}; do
+    env "${v#*=}" timeout -k 10 300 $B > $OUT/bench_${v%%=*}_$r.log 2>&1 || exit 1
+  done
 done
 python scripts/ab_summary.py ${RUN:-libab} || true
