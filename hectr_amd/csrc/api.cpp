@@ -801,6 +801,17 @@ extern "C" void he_mul_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt)
   out->flags = 0;
 }
 
+// Where the fused path adds the tensor terms d0/d1 of the keep limbs: in the
+// key switch's accumulator as P (d0, d1) (default: ks_rows2's loads overlap
+// its latency-bound row passes) or in the ModDown epilogue after the division
+// (GPQHE_D01_KS=0; dn_rows is HBM-bound).  Same-box A/B at N=2^16, L=8:
+// 31.1k vs 30.1k ct-mult/s (ks_rows2 +120 us, dn_rows -215 us per chunk).
+static bool d01_in_ks()
+{
+  const char *e = getenv("GPQHE_D01_KS");
+  return !e || atoi(e);
+}
+
 // Tensor + relinearize [+ rescale] for `count` ciphertext pairs.
 //   a, b: ciphertext i at a + i*in_stride, c1 at + in_pstride;
 //   out:  polynomial p (= 2 i + {0,1}) at out + p*out_pstride.
@@ -832,12 +843,14 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
     // keep slots' MAC deferred into the ModDown rows (kd_rows_kernel)
     const bool defer = dn_fused && k_ks_defer_ok(lvl);
     const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
+    const bool dks = dn_fused && !defer && d01_in_ks();
     const D01Src src = k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride, evkm, count,
-                                             lvl, dn_fused ? keep : 0, dn_fused ? keep : nm, lazy,
+                                             lvl, dn_fused && !dks ? keep : 0, dn_fused ? keep : nm, lazy,
                                              defer ? keep : 0);
     if (dn_fused) {
       const KsDeferred ks{D.p, d2.p, evkm};
-      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, src, nullptr, defer ? &ks : nullptr);
+      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, dks ? D01Src{} : src, nullptr,
+                      defer ? &ks : nullptr);
       return;
     }
   } else {
@@ -869,15 +882,15 @@ static void mul_chunk_fused(const LaneWs &w, uint64_t *out, size_t out_pstride, 
   const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
   const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
   auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
-  const bool defer = k_ks_defer_ok(lvl);
+  const bool defer = k_ks_defer_ok(lvl), dks = !defer && d01_in_ks();
   const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
   const D01Src src = k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride, evkm, count,
-                                           lvl, keep, keep,
+                                           lvl, dks ? 0 : keep, keep,
                                            !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) &&
                                                !overlap(b),
                                            defer ? keep : 0);
   const KsDeferred ks{w.T1, w.d2, evkm};
-  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, src, w.conv,
+  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, dks ? D01Src{} : src, w.conv,
                   defer ? &ks : nullptr);
 }
 

@@ -1482,6 +1482,50 @@ __device__ __forceinline__ void d01_fetch8(const D01Src &s, unsigned P, size_t o
   }
 }
 
+// f0 += P d0, f1 += P d1 of pair i at words off .. off + 7 (8 consecutive
+// words, 16-byte loads), in FP64 for m.q < 2^51 (caller's guarantee).  Bounds:
+// f0, f1 arrive with |.| < 3q (two MAC products); they are reduced to
+// |.| <= q/2 first, d0 = a0 b0 is < 1.25 q, d1 = a0 b1 + a1 b0 is reduced to
+// <= q/2, and each P d term is < 1.5 q, so every value stays an exact integer
+// below 2^53 and the results are < 2q (canonicalised by the caller).
+__device__ __forceinline__ void d01_fold_f64(const D01Src &s, unsigned i, size_t off, const ModConst &m,
+                                             double (&f0)[8], double (&f1)[8])
+{
+  const double q = (double)m.q, qinv = 1.0 / q, P = f64_from_u52(m.pmod), Pq = P * qinv;
+  auto ld8 = [](const uint64_t *src, double (&x)[8]) {
+    const ulonglong2 *v2 = (const ulonglong2 *)src;
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      const ulonglong2 w = v2[h];
+      x[2 * h] = f64_from_u52(w.x);
+      x[2 * h + 1] = f64_from_u52(w.y);
+    }
+  };
+  double d0[8], d1[8];
+  if (s.d01) {
+    ld8(s.d01 + (2 * i) * s.pstride + off, d0);
+    ld8(s.d01 + (2 * i + 1) * s.pstride + off, d1);
+  } else {
+    double a0[8], a1[8], b0[8], b1[8];
+    const uint64_t *pa = s.a + i * s.in_stride + off, *pb = s.b + i * s.in_stride + off;
+    ld8(pa, a0);
+    ld8(pb, b0);
+    ld8(pa + s.in_pstride, a1);
+    ld8(pb + s.in_pstride, b1);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      d0[k] = f64_mulmod(a0[k], b0[k], b0[k] * qinv, q);
+      d1[k] = f64_red(f64_mulmod(a0[k], b1[k], b1[k] * qinv, q) + f64_mulmod(a1[k], b0[k], b0[k] * qinv, q), q,
+                      qinv);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    f0[k] = f64_red(f0[k], q, qinv) + f64_mulmod(d0[k], P, Pq, q);
+    f1[k] = f64_red(f1[k], q, qinv) + f64_mulmod(d1[k], P, Pq, q);
+  }
+}
+
 // Tensor of count ciphertext pairs: d0 = a0 b0, d1 = a0 b1 + a1 b0 into
 // d01 [count][2][lvl][n]; d2 = a1 b1 into d2 [count][lvl][n].  Two adjacent
 // coefficients per thread (16-byte accesses).  Moduli below 2^51 use the exact
@@ -2880,7 +2924,12 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
           }
         }
       }
+      bool folded = false;  // P (d0, d1) added in FP64 before canonicalising
       if constexpr (std::is_same<A, ArF64>::value) {
+        if (t < lvl && t >= p_lo) {
+          d01_fold_f64(d01, p, ((size_t)t << logn) + toff + 8 * th, mc, f0, f1);
+          folded = true;
+        }
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           a0[k] = ar.canon(f0[k]);
@@ -2895,7 +2944,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         (void)f0;
         (void)f1;
       }
-      if (t < lvl && t >= p_lo) {
+      if (!folded && t < lvl && t >= p_lo) {
         // round C ownership is natural order: words 8 th .. 8 th + 7
         int pos[8];
 #pragma unroll
@@ -3580,7 +3629,14 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
     pos[i] = wl_elem(i);
     xv[i] = xs[pos[i]];
   }
-  d01_fetch8(d01, p, toff, pos, mc, dv);
+  if (d01.d01 || d01.a) {
+    d01_fetch8(d01, p, toff, pos, mc, dv);
+  } else {
+    // no d0/d1 source: the key switch added P (d0, d1) to X already (p_lo = 0)
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      dv[i] = 0;
+  }
   uint64_t cv[8];
   with_arith(q, m, logn, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
@@ -3825,7 +3881,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
   }
   // reads conv, X and the d0/d1 source (one limb, or lazily the products'
   // factors: a0 b0 for d0, a0 a1 b0 b1 for d1), writes out
-  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * (d01.d01 ? 4.0 : 6.0));
+  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * (d01.d01 ? 4.0 : d01.a ? 6.0 : 3.0));
   hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
                      out, out_pstride, X, x_pstride, d01, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
