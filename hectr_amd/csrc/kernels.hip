@@ -3002,9 +3002,15 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
                             const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
-                            unsigned drop_lo, unsigned t_lo, bool rowform)
+                            unsigned drop_lo, unsigned t_lo, bool rowform, bool invc)
 {
-  UpTable &tab = up_table(lvl);
+  // invc: y holds only the inverse row pass of d2 (d2_rows_kernel, unscaled);
+  // ks_cols4 runs the inverse column pass with the full n^-1 [(Qj/q_i)^-1]
+  UpTable tab = up_table(lvl);
+  if (invc && !rowform)
+    tab.ysc1 = tab.ysc;
+  rowform = rowform || invc;  // (the ks_cols4 form; ks_rows2 keeps own_rowform below)
+  const bool own_rowform = rowform && !invc;
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
   const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
                acc_stride = 2 * (size_t)nm * n;
@@ -3059,12 +3065,12 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
                        t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, t_lo, rowform ? 1 : 0, tw,
+                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, t_lo, own_rowform ? 1 : 0, tw,
                        G.dev.mc, g_ablate);
   } else {
     hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
                        T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, ndig, G.alpha, count, p_lo, drop_lo, rowform ? 1 : 0, tw, G.dev.mc);
+                       G.nmod, ndig, G.alpha, count, p_lo, drop_lo, own_rowform ? 1 : 0, tw, G.dev.mc);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -3114,6 +3120,15 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   with_arith(mc.q, limb, logn, tw, [&](const auto &ar) { rows8_tile_raw<LOGN2, true>(ar, raw, yo, lds, n1 + row0); });
 }
 
+// Default on (GPQHE_KSC_INVC=0: separate ntt2_cols pass).  Same-box A/B at
+// N=2^16, L=8: 31.4k vs 30.7k ct-mult/s (ks_cols4 +80 us, ntt2_cols -128 us
+// per chunk: the column INTT is done once per digit tile, NT = 8 targets).
+static bool ks_invc()
+{
+  const char *e = getenv("GPQHE_KSC_INVC");
+  return !e || atoi(e);
+}
+
 bool k_ks_fused_ok()
 {
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
@@ -3138,7 +3153,7 @@ bool k_ks_defer_ok(unsigned lvl)
 // [count][2][lvl] too unless lazy (then d0/d1 come from a and b, D01Src).
 template <int LOGT1, int LOGN2>
 static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, const uint64_t *b, size_t in_stride,
-                           size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab)
+                           size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab, bool cols)
 {
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned n = G.n;
@@ -3148,6 +3163,8 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
     hipLaunchKernelGGL((d2_rows_kernel<LOGN2>), dim3(lvl * count * (n / 2048)), dim3(256), 0, G.stream, d2, ybuf, a,
                        b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc);
   }
+  if (!cols)  // the column pass runs inside ks_cols4 (invc)
+    return;
   LimbSet ys{};
   ys.base = ybuf;
   ys.stride = (size_t)lvl * n;
@@ -3175,6 +3192,9 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
     gpqhe_die("k_mul_keyswitch_fused: the row form needs the d01 buffer (lazy = false)");
   if (rowform && t_lo)
     gpqhe_die("k_mul_keyswitch_fused: deferred slots need the NTT-form d2 limbs (no row form)");
+  // invc: the d2 INTT's column pass runs inside ks_cols4 (one block per digit
+  // tile and all its targets) instead of a separate ntt2_cols pass (A/B switch)
+  const bool invc = lazy && !rowform && G.alpha <= 4 && G.logn <= 16 && ks_invc();
   D01Src src{lazy ? nullptr : d01, (size_t)lvl * G.n, a, b, in_stride, in_pstride};
   if (rowform) {
     // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
@@ -3184,11 +3204,11 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
       tensor_rows_launch<7>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
   } else if (lazy) {
     switch (G.logn) {
-    case 13: d2_intt_launch<6, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
-    case 14: d2_intt_launch<7, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
-    case 15: d2_intt_launch<7, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
-    case 16: d2_intt_launch<8, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
-    case 17: d2_intt_launch<8, 9>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab); break;
+    case 13: d2_intt_launch<6, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+    case 14: d2_intt_launch<7, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+    case 15: d2_intt_launch<7, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+    case 16: d2_intt_launch<8, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+    case 17: d2_intt_launch<8, 9>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
     default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
     }
   } else {
@@ -3205,11 +3225,11 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
   }
   const uint64_t *y = rowform ? d2 : ybuf;
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
-  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
-  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
-  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
-  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform); break;
+  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
+  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
+  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
+  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
+  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
   }
   return src;

@@ -171,7 +171,8 @@ def test_ntt_batch_bitexact(oracle, product, name):
 @pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51",
                                   "bench51_tensor", "c5", "c17", "c14", "c15", "bench_d2_kd", "bench51_kd",
                                   "bench51_tensor_kd", "c14_kd", "c15_kd", "c17_kd", "bench_d2_dnd",
-                                  "bench51_dnd", "bench51_tensor_dnd", "c15_dnd", "c5_dnd"])
+                                  "bench51_dnd", "bench51_tensor_dnd", "c15_dnd", "c5_dnd",
+                                  "bench_d2_noinvc", "bench51_noinvc", "c14_noinvc", "c15_noinvc"])
 def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
     latter also through the opt-in row-form key switch and through the
@@ -186,6 +187,9 @@ def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
     if name.endswith("_kd"):
         monkeypatch.setenv("GPQHE_KDROWS", "1")
         name = name[:-len("_kd")]
+    if name.endswith("_noinvc"):  # d2's INTT columns in ntt2_cols, not ks_cols4 (GPQHE_KSC_INVC=0)
+        monkeypatch.setenv("GPQHE_KSC_INVC", "0")
+        name = name[:-len("_noinvc")]
     if name.endswith("_dnd"):  # d0/d1 added in the ModDown epilogue (GPQHE_D01_KS=0)
         monkeypatch.setenv("GPQHE_D01_KS", "0")
         name = name[:-len("_dnd")]
