@@ -3055,7 +3055,8 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     gpqhe_die("deferred key-switch slots need the two-digit ks_rows2 path");
   const double ns = nm - t_lo;
   ProfScope ps(rows2 ? KC_KS_ROWS2 : KC_KS_ROWS,
-               8.0 * n * ((double)count * (ndig * ns + 2.0 * (lvl - std::min(p_lo, lvl)) + 2 * ns) +
+               8.0 * n * ((double)count * (ndig * ns + (d01.d01 ? 2.0 : 4.0) * (lvl - std::min(p_lo, lvl)) +
+                                           2 * ns) +
                           2.0 * ndig * ns));
   if (rows2) {
     // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
@@ -3194,7 +3195,11 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_
     gpqhe_die("k_mul_keyswitch_fused: deferred slots need the NTT-form d2 limbs (no row form)");
   // invc: the d2 INTT's column pass runs inside ks_cols4 (one block per digit
   // tile and all its targets) instead of a separate ntt2_cols pass (A/B switch)
-  const bool invc = lazy && !rowform && G.alpha <= 4 && G.logn <= 16 && ks_invc();
+  // (one ks_cols4 block must own all of a digit's targets, else the column
+  // INTT repeats per block: config 5, 12 targets per digit, measured 7.6k vs
+  // 7.8k ct-mult/s, so it keeps the separate pass)
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, na_min = lvl - (ndig - 1) * G.alpha;
+  const bool invc = lazy && !rowform && G.alpha <= 4 && tab.nm - na_min <= 8 && ks_invc();
   D01Src src{lazy ? nullptr : d01, (size_t)lvl * G.n, a, b, in_stride, in_pstride};
   if (rowform) {
     // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
