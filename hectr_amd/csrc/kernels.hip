@@ -639,10 +639,12 @@ __device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn
 }
 
 // FP64 basis conversion per kernel (GPQHE_FBC64 bit mask, timing studies):
-// 1 ks_cols4, 2 dn_cols.  Both are exact; the mask only selects the faster one.
+// 1 ks_cols4 with the INVC column pass, 2 dn_cols, 4 ks_cols4 NT = 4.  All are
+// exact; the mask only selects the faster form (same box: INVC ks_cols4 323 vs
+// 388 us per chunk with FP64; NT = 4 ks_cols4 488 vs 308 us with FP64).
 static int fbc64_mask()
 {
-  static const int m = getenv("GPQHE_FBC64") ? atoi(getenv("GPQHE_FBC64")) : 2;
+  static const int m = getenv("GPQHE_FBC64") ? atoi(getenv("GPQHE_FBC64")) : 3;
   return m;
 }
 
@@ -3040,7 +3042,7 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
         hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
                            t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
       };
-      tab.f64 && (fbc64_mask() & 1) ? go(ks_cols4_kernel<LOGT1, NT, false, true>)
+      tab.f64 && (fbc64_mask() & 4) ? go(ks_cols4_kernel<LOGT1, NT, false, true>)
                                     : go(ks_cols4_kernel<LOGT1, NT, false, false>);
     } else {
       hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
@@ -3062,7 +3064,10 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
     // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
     const unsigned groups = (nm - t_lo) * (n / 2048);
     static const unsigned want = getenv("GPQHE_KSR_MEMBERS") ? atoi(getenv("GPQHE_KSR_MEMBERS")) : 0;
-    const unsigned members = std::max(1u, std::min(count, want ? want : (6 * 256 + groups - 1) / groups));
+    // runs of about 8 ciphertexts per block (64 pairs: 693 vs 712 us for runs
+    // of 13), more and shorter runs when the batch is too small to fill the GPU
+    const unsigned fill = std::min(count, (6 * 256 + groups - 1) / groups);
+    const unsigned members = std::max(1u, want ? std::min(count, want) : std::max((count + 7) / 8, fill));
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
                        t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
