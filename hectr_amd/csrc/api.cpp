@@ -1098,11 +1098,13 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
   const size_t per_ct = (size_t)(2 * lvl + 2 * lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
-  // workspace per chunk (GPQHE_WS_MIB, default 4 GiB: 86 pairs at N=2^16, L=8,
-  // dnum=2).  Bigger chunks fill the GPU better (dn_cols has 32 blocks per
-  // pair) and amortize ks_rows2's key tiles over longer runs: same-box A/B
-  // 27.3k (2 GiB) vs 28.3-28.6k (2.5-4 GiB); 288 GB of HBM leave room.
-  static const size_t budget = (size_t)env_u("GPQHE_WS_MIB", 4096) << 20;
+  // workspace per chunk (GPQHE_WS_MIB, default 8 GiB: 170 pairs at N=2^16, L=8,
+  // dnum=2, so the bench's 256 pairs run as 2 chunks of 128).  Bigger chunks
+  // fill the GPU better (dn_cols has 32 blocks per pair) and amortize
+  // ks_rows2's key tiles over more runs: same-box A/B 27.3k (2 GiB) vs
+  // 28.3-28.6k (2.5-4 GiB); later 32.3-32.7k (4 GiB) vs 33.5k (8 GiB) vs
+  // 33.3k (16 GiB, one chunk).  288 GB of HBM leave room.
+  static const size_t budget = (size_t)env_u("GPQHE_WS_MIB", 8192) << 20;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));
   if (const char *e = getenv("GPQHE_CHUNK"))  // test hook: force small chunks (several lanes' worth)
