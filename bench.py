@@ -144,7 +144,7 @@ def main():
         achieved = nbytes / tot_us / 1e3  # GB/s
         workload = (f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, dnum={eng.info.dnum}, "
                     f"primes {args.q0_bits}/50/{args.p_bits} bits, batch={B} pairs per GPU")
-        traffic, src = pmc_traffic(dom_name, workload)
+        traffic, src = pmc_traffic(dom_name, workload, tot_us / launches)
         dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                "avg_launch_us": tot_us / launches, "alg_bytes_per_launch": nbytes / launches,
@@ -194,12 +194,15 @@ def main():
     return result
 
 
-def pmc_traffic(kernel, workload):
+def pmc_traffic(kernel, workload, avg_us):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc.json, written by scripts/prof_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload, with
-    the gfx950 FETCH_SIZE x2 correction).  (None, None) when no profile of this
-    workload exists: PMC counters cannot be read from inside the timed run."""
+    the gfx950 FETCH_SIZE x2 correction).  A profile whose mean launch time is
+    not within 0.7-1.4x of this run's (`avg_us`) was taken with another chunk
+    size, so its bytes per launch do not apply and it is skipped.  (None, None)
+    when no profile of this workload exists: PMC counters cannot be read from
+    inside the timed run."""
     import glob
     import re
     def order(f):  # profiles/r<round>_v<version>_pmc.json, newest first
@@ -219,6 +222,8 @@ def pmc_traffic(kernel, workload):
             if name.split("<")[0] != base or "hbm_bytes" not in e:
                 continue
             if flag and not name.endswith(flag):
+                continue
+            if not 0.7 <= e.get("mean_us", avg_us) / avg_us <= 1.4:
                 continue
             return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
     return None, None
