@@ -7,33 +7,46 @@ one step = one batch through he_mul_rescale_batch).  Inputs are synthetic
 random-residue ciphertexts already resident in HBM (poly_fill_uniform,
 splitmix64 streams); the relinearization key is a real key (he_genrlk).
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL), each rank
-multiplies its own batch (independent ciphertexts: no data-path
-collective); the collective is only the barrier / max-time reduction.
-`value` = pairs processed by all ranks / max rank time ("scaling": "weak").
+Multi-GPU: one process per GPU, each rank multiplies its own
+batch (independent ciphertexts: no data-path collective; RCCL carries only
+the barrier and the max-time reduction).  `value` = pairs processed by all
+ranks / max rank time ("scaling": "weak").  Under torchrun the ranks come from
+the environment; `--gpus N` without torchrun starts the N rank processes
+itself, before anything touches the GPU.
 
-Also reported on rank 0:
-  roofline      - for the dominant kernel, algorithmic bytes per launch /
-                  its average launch duration (HIP events on the engine
-                  stream, same shapes as inside the step), vs 8 TB/s;
-  cpu_baseline  - the CPU restatement (oracle/, "port") timed on this host
-                  on a bounded sample of the same op;
-  op_roofline   - the whole op against its algorithmic bytes (24.4 MB/op).
+Also reported (rank 0):
+  roofline      - the dominant kernel: SURVEY 8(d)'s algorithmic bytes per op
+                  (2 ct in, 1 ct out at L-1, key / batch) x the pairs one launch
+                  processes, / its average launch time (HIP events on the
+                  engine stream), vs 8 TB/s; the kernel's own streamed bytes
+                  and the PMC traffic of the pipeline beside it;
+  op_roofline   - the whole op against its algorithmic bytes;
+  value_60bit   - the same op with the conventional 60-bit q0 / special primes;
+  config5       - n=2^17, L=12 (dnum 3, K 4), per GPU and aggregate;
+  ntt_roundtrip - config 2 (1024 polys, forward + inverse, identity checked);
+  cstr          - config 4, the encrypted CSTR-MPC loop;
+  cpu_baseline  - the CPU restatement (oracle/, "port") on this host.
 """
 import argparse
 import ctypes
+import glob
 import json
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# kernels of the fused he_mul_rescale_batch pipeline (n = 2^16: one launch each per chunk)
+PIPELINE = ("d2_rows_kernel", "ks_cols4_kernel", "ks_rows2_kernel", "dn_cols_kernel", "dn_rows_kernel")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -52,226 +65,196 @@ def parse():
     ap.add_argument("--cstr-steps", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT roundtrip leg (config 2)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config 5 leg (n=2^17, L=12)")
+    ap.add_argument("--c5-batch", type=int, default=64)
     ap.add_argument("--ntt-polys", type=int, default=1024)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample duration")
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample duration per thread count")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="run only the multi-process launch / rendezvous / reduction path (no engine, no GPU)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------
+# Launch: torchrun, or N rank processes started here
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
+
+def spawn_ranks(n):
+    """Start n fresh rank processes of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set) and wait for them.  The parent never touches the
+    GPU, so no process that initialised it is ever replaced.  Returns the
+    first non-zero exit code (0 when all ranks succeeded)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c), 0)
+
+
+def launch_check(args):
+    """The N > 1 harness without the engine: rendezvous, barrier, the
+    max-over-ranks reduction bench.py times with, and rank 0's JSON line."""
     from hectr_amd import dist as hdist
-    from hectr_amd.gpqhe import Engine
-
-    rank, world, local = hdist.env()
-    # one process per GPU; the modulus only matters for rehearsals with more
-    # ranks than GPUs (HECTR_DIST_BACKEND=gloo: RCCL needs distinct devices)
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    rank, world, _ = hdist.env()
     backend = os.environ.get("HECTR_DIST_BACKEND", "nccl")
     hdist.init(backend)
-    red_dev = "cuda" if backend == "nccl" else "cpu"
-    barrier = hdist.barrier
-
-    L, logn, B = args.nlimbs, args.logn, args.batch
-    n = 1 << logn
-    dnum = args.dnum or L
-    K = args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits, p_bits=args.p_bits)
-    eng = Engine.product()
-    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=args.q0_bits, qi_bits=50,
-                    p_bits=args.p_bits, seed=1000 + rank)
-    stream = torch.cuda.Stream()
-    eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
-    pk, sk, rlk = eng.pk(), eng.sk(), eng.evk()
-    eng.keypair(pk, sk)
-    eng.genrlk(rlk, sk)
-    in_words, out_words = 2 * L * n, 2 * (L - 1) * n
-    a = torch.empty(B * in_words, dtype=torch.int64, device="cuda")
-    b = torch.empty_like(a)
-    out = torch.empty(B * out_words, dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    # global pairs [rank B, (rank + 1) B): each rank multiplies its own shard
-    hdist.fill_pairs(eng.lib, a.data_ptr(), b.data_ptr(), rank * B, B, L, n)
-    eng.sync()
-
-    def step():
-        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
-
-    for _ in range(args.warmup):
-        step()
-    eng.sync()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    eng.sync()
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    ev_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = hdist.max_over_ranks(elapsed, device=red_dev)
-    ops = world * B * args.steps
-    value = ops / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
-
-    # algorithmic bytes per op: 2 ct in, 1 ct out at L-1, rlk amortised over the batch
-    evk_bytes = 2 * eng.info.dnum * (L + K) * n * 8
-    alg_bytes = (2 * in_words + out_words) * 8 + evk_bytes / B
-
-    # instrumented pass (same steps): per-kernel device time from HIP events on
-    # the engine stream, algorithmic bytes per launch from the library
-    eng.prof_enable(True)
-    ti0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    eng.sync()
-    ti1 = time.perf_counter()
-    stats = eng.prof_collect()
-    eng.prof_enable(False)
-
-    result = None
+    hdist.barrier()
+    t = hdist.max_over_ranks(float(rank + 1))
     if rank == 0:
-        dom_name = max(stats, key=lambda k: stats[k][1])
-        launches, tot_us, nbytes = stats[dom_name]
-        achieved = nbytes / tot_us / 1e3  # GB/s
-        workload = (f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={K}, dnum={eng.info.dnum}, "
-                    f"primes {args.q0_bits}/50/{args.p_bits} bits, batch={B} pairs per GPU")
-        traffic, src = pmc_traffic(dom_name, workload, tot_us / launches)
-        dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
-               "avg_launch_us": tot_us / launches, "alg_bytes_per_launch": nbytes / launches,
-               "share_of_step": tot_us / (1e6 * (ti1 - ti0))}
-        kernels = {k: {"launches": v[0], "avg_us": v[1] / v[0], "share": v[1] / (1e6 * (ti1 - ti0)),
-                       "GBs": v[2] / v[1] / 1e3} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
-        result = {
-            "metric": "ct×ct+relin/sec at N=2^16, L=8 RNS primes; encrypted CSTR-MPC steps/sec",
-            "value": value,
-            "unit": "ct-mult/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic random-residue ciphertexts (splitmix64), real relinearization key",
-            "config": {"workload": workload,
-                       "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": K,
-                       "dnum": eng.info.dnum, "prime_bits": {"q0": args.q0_bits, "qi": 50, "p": args.p_bits},
-                       "parallelism": f"batch-sharded x{world}"},
-            "event_s_rank0": ev_s,
-            "op_roofline": {"alg_bytes_per_op": alg_bytes,
-                            "achieved_GBs": alg_bytes * value / world / 1e9,
-                            "frac": alg_bytes * value / world / 1e9 / HBM_PEAK_GBS},
-            "roofline": dom,
-            "kernels": kernels,
-            "instrumented_ms_per_step": 1e3 * (ti1 - ti0) / args.steps,
-        }
-    if rank == 0 and not args.no_ntt:
-        result["ntt_roundtrip"] = ntt_roundtrip(eng, stream, logn, L, args.ntt_polys)
-    if rank == 0 and world == 1 and args.alt_bits and args.alt_bits != args.q0_bits:
-        eng.exit()
-        result["alt_primes"] = alt_rate(args, stream, L, logn, B, dnum)
-    barrier()
-    if rank == 0 and not args.no_cstr:
-        eng.exit()
-        result["cstr"] = cstr_loop(args.cstr_steps)
-    if rank == 0 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, logn, L, dnum)
-    if rank == 0:
-        print(json.dumps(result))
+        print(json.dumps({"launch_check": True, "n_gpus": world, "requested": args.gpus, "max_over_ranks": t}))
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
-    return result
 
 
-def pmc_traffic(kernel, workload, avg_us):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*_pmc.json, written by scripts/prof_summary.py from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload, with
-    the gfx950 FETCH_SIZE x2 correction).  A profile whose mean launch time is
-    not within 0.7-1.4x of this run's (`avg_us`) was taken with another chunk
-    size, so its bytes per launch do not apply and it is skipped.  (None, None)
-    when no profile of this workload exists: PMC counters cannot be read from
-    inside the timed run."""
-    import glob
-    import re
+# ---------------------------------------------------------------------------
+# Timed legs
+# ---------------------------------------------------------------------------
+def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):
+    """Smallest K with P = prod(p_i) above the largest digit modulus (hybrid
+    key switching needs P > Q_j for its noise bound)."""
+    alpha = -(-L // dnum)
+    digit_bits = q0_bits + (alpha - 1) * qi_bits
+    return max(1, -(-digit_bits // p_bits))
+
+
+def alg_bytes_per_op(n, L, K, dnum, batch):
+    """read 2 ct (2 L limbs each), write 1 ct at L-1, the
+    relinearization key (2 dnum (L+K) limbs) amortised over the batch."""
+    return (2 * 2 * L + 2 * (L - 1)) * n * 8 + 2 * dnum * (L + K) * n * 8 / batch
+
+
+class MulBatch:
+    """One engine context + resident inputs for he_mul_rescale_batch."""
+
+    def __init__(self, stream, logn, L, dnum, q0_bits, p_bits, nspecial, batch, first, seed):
+        import torch
+        from hectr_amd import dist as hdist
+        from hectr_amd.gpqhe import Engine
+        self.K = nspecial or special_primes(L, dnum, q0_bits=q0_bits, p_bits=p_bits)
+        self.eng = Engine.product()
+        self.eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=self.K, slots=64, q0_bits=q0_bits,
+                             qi_bits=50, p_bits=p_bits, seed=seed)
+        self.eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
+        self.pk, self.sk, self.rlk = self.eng.pk(), self.eng.sk(), self.eng.evk()
+        self.eng.keypair(self.pk, self.sk)
+        self.eng.genrlk(self.rlk, self.sk)
+        n = 1 << logn
+        self.n, self.L, self.B, self.dnum = n, L, batch, self.eng.info.dnum
+        self.a = torch.empty(batch * 2 * L * n, dtype=torch.int64, device="cuda")
+        self.b = torch.empty_like(self.a)
+        self.out = torch.empty(batch * 2 * (L - 1) * n, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        # global pairs [first, first + batch): each rank multiplies its own shard
+        hdist.fill_pairs(self.eng.lib, self.a.data_ptr(), self.b.data_ptr(), first, batch, L, n)
+        self.eng.sync()
+
+    def step(self):
+        self.eng.lib.he_mul_rescale_batch(self.out.data_ptr(), self.a.data_ptr(), self.b.data_ptr(), self.B, self.L,
+                                          ctypes.byref(self.rlk))
+
+    def alg_bytes(self):
+        return alg_bytes_per_op(self.n, self.L, self.K, self.dnum, self.B)
+
+    def close(self):
+        del self.a, self.b, self.out
+        self.eng.exit()
+
+
+def timed(fn, steps, warmup, sync, barrier):
+    """W untimed steps, then K timed steps bracketed by barrier + device sync."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    sync()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def pmc_profile(workload, pairs_per_launch):
+    """Newest committed PMC summary (profiles/*_pmc.json, scripts/prof_summary.py
+    over separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same
+    workload) whose metadata records the same pairs per launch."""
     def order(f):  # profiles/r<round>_v<version>_pmc.json, newest first
         m = re.search(r"r(\d+)_v(\d+)_pmc", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order, reverse=True)
-    for f in files:
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order, reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("meta", {}).get("bench_workload") != workload:
-            continue
-        base, _, tag = kernel.partition("<")
-        flag = {"fwd>": "false>", "inv>": "true>"}.get(tag)
-        for name, e in d.get("kernels", {}).items():
-            if name.split("<")[0] != base or "hbm_bytes" not in e:
-                continue
-            if flag and not name.endswith(flag):
-                continue
-            if not 0.7 <= e.get("mean_us", avg_us) / avg_us <= 1.4:
-                continue
-            return e["hbm_bytes"], os.path.relpath(f, ROOT) + ":" + name
+        meta = d.get("meta", {})
+        if meta.get("bench_workload") == workload and meta.get("pairs_per_launch") == pairs_per_launch:
+            return d, os.path.relpath(f, ROOT)
     return None, None
 
 
-def alt_rate(args, stream, L, logn, B, dnum):
-    """The same op and batch with q0 and the special primes at args.alt_bits
-    (60: the conventional CKKS sizes).  Limbs of 51 bits and more take the
-    64-bit integer butterflies instead of the FP64 ones."""
-    from hectr_amd.gpqhe import Engine
-    bits = args.alt_bits
-    K = special_primes(L, dnum, q0_bits=bits, p_bits=bits)
-    eng = Engine.product()
-    eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=K, slots=64, q0_bits=bits, qi_bits=50, p_bits=bits,
-                    seed=1000)
-    eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
-    pk, sk, rlk = eng.pk(), eng.sk(), eng.evk()
-    eng.keypair(pk, sk)
-    eng.genrlk(rlk, sk)
-    import torch
-    n = 1 << logn
-    a = torch.empty(B * 2 * L * n, dtype=torch.int64, device="cuda")
-    b = torch.empty_like(a)
-    out = torch.empty(B * 2 * (L - 1) * n, dtype=torch.int64, device="cuda")
-    from hectr_amd import dist as hdist
-    hdist.fill_pairs(eng.lib, a.data_ptr(), b.data_ptr(), 0, B, L, n)
-    for _ in range(max(1, args.warmup)):
-        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
-    eng.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.lib.he_mul_rescale_batch(out.data_ptr(), a.data_ptr(), b.data_ptr(), B, L, ctypes.byref(rlk))
-    eng.sync()
-    dt = time.perf_counter() - t0
-    eng.exit()
-    return {"q0_bits": bits, "qi_bits": 50, "p_bits": bits, "nspecial": K, "value": B * args.steps / dt,
-            "unit": "ct-mult/s", "steps": args.steps}
+def pmc_entry(prof, kernel):
+    base = kernel.split("<")[0]
+    for name, e in prof.get("kernels", {}).items():
+        if name.split("<")[0] == base and "hbm_bytes" in e:
+            return e
+    return None
+
+
+def roofline(stats, total_s, mb, workload, pairs_per_launch):
+    dom_name = max(stats, key=lambda k: stats[k][1])
+    launches, tot_us, kbytes = stats[dom_name]
+    avg_us = tot_us / launches
+    alg = mb.alg_bytes() * pairs_per_launch
+    achieved = alg / avg_us / 1e3  # GB/s
+    prof, src = pmc_profile(workload, pairs_per_launch)
+    e = pmc_entry(prof, dom_name) if prof else None
+    dom = {"bound": "hbm", "kernel": dom_name, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": e["hbm_bytes"] if e else None,
+           "traffic_source": src, "avg_launch_us": avg_us, "alg_bytes_per_launch": alg,
+           "alg_basis": f"SURVEY 8(d): {mb.alg_bytes():.0f} B/op x {pairs_per_launch} pairs per launch",
+           "kernel_streamed_bytes_per_launch": kbytes / launches,
+           "kernel_streamed_GBs": kbytes / tot_us / 1e3,
+           "share_of_step": tot_us / (1e6 * total_s)}
+    if e:
+        for k in ("valu_busy", "sq_wait_any", "mean_us"):
+            if k in e:
+                dom["pmc_" + k] = e[k]
+    if prof:
+        pipe = [pmc_entry(prof, k) for k in PIPELINE]
+        if all(pipe):
+            tot = sum(p["hbm_bytes"] for p in pipe)
+            dom["pipeline_traffic_per_chunk"] = tot
+            dom["pipeline_traffic_ratio"] = tot / alg
+    return dom
 
 
 def ntt_roundtrip(eng, stream, logn, L, polys, reps=3):
     """Config 2: forward + inverse NTT of `polys` polynomials x L limbs at
     N=2^logn resident in HBM (poly_ntt_batch / poly_intt_batch), timed with
     HIP events on the engine stream; algorithmic bytes = read + write of every
-    limb per transform (twiddles amortised), i.e. 16 n L bytes per poly."""
+    limb per transform (twiddles amortised), i.e. 16 n L bytes per poly per
+    transform.  The roundtrip identity is checked on the whole batch."""
     import torch
     n = 1 << logn
     buf = torch.empty(polys * L * n, dtype=torch.int64, device="cuda")
     eng.lib.poly_fill_uniform(buf.data_ptr(), polys, L, 0x48454354520001)
+    eng.sync()
+    orig = buf.clone()  # (on torch's stream: wait for it before the engine stream runs)
+    torch.cuda.synchronize()
     eng.lib.poly_ntt_batch(buf.data_ptr(), polys, L)
     eng.lib.poly_intt_batch(buf.data_ptr(), polys, L)
     eng.sync()
@@ -283,18 +266,11 @@ def ntt_roundtrip(eng, stream, logn, L, polys, reps=3):
     ev1.record(stream)
     eng.sync()
     dt = ev0.elapsed_time(ev1) / 1e3 / reps
+    identity = bool(torch.equal(buf, orig))
     alg = 2.0 * 2 * 8 * n * L * polys  # two transforms, each reads + writes every limb once
-    del buf
+    del buf, orig
     return {"polys": polys, "nlimbs": L, "logn": logn, "roundtrip_ms": 1e3 * dt, "polys_per_s": polys / dt,
-            "alg_GBs": alg / dt / 1e9, "frac_of_8TBs": alg / dt / 8e12}
-
-
-def special_primes(L, dnum, q0_bits=60, qi_bits=50, p_bits=60):
-    """Smallest K with P = prod(p_i) above the largest digit modulus (hybrid
-    key switching needs P > Q_j for its noise bound)."""
-    alpha = -(-L // dnum)
-    digit_bits = q0_bits + (alpha - 1) * qi_bits
-    return max(1, -(-digit_bits // p_bits))
+            "alg_GBs": alg / dt / 1e9, "frac_of_8TBs": alg / dt / 8e12, "identity_ok": identity}
 
 
 def cstr_loop(steps):
@@ -321,39 +297,192 @@ def cstr_loop(steps):
             "max_rel_dev_vs_plaintext": rel}
 
 
+def usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, logn, L, dnum):
-    """Oracle (CPU restatement, -O3, OpenMP over the batch) on a bounded
-    sample of the same op; threads = OMP_NUM_THREADS (16 on the GPU box)."""
+    """The oracle (CPU restatement, -O3, OpenMP over the batch) on a bounded
+    sample of the same op, at the host's CPU share (OMP_NUM_THREADS: 16 on
+    the GPU box) and at 4 threads (the reference's GPQHE_NUM_THREAD,
+    src/config.h:59).  `value` is the first."""
     import numpy as np
 
     from hectr_amd.gpqhe import Engine
-    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    share = int(os.environ.get("OMP_NUM_THREADS", str(min(16, usable_cpus()))))
+    gomp = ctypes.CDLL("libgomp.so.1")
     ora = Engine.oracle()
+    K = args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits, p_bits=args.p_bits)
     ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=64, q0_bits=args.q0_bits, qi_bits=50, p_bits=args.p_bits,
-                    seed=7, nspecial=args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits,
-                                                                     p_bits=args.p_bits))
+                    seed=7, nspecial=K)
     pk, sk, rlk = ora.pk(), ora.sk(), ora.evk()
     ora.keypair(pk, sk)
     ora.genrlk(rlk, sk)
     n = 1 << logn
-    cnt = 4 * threads  # a fixed set of pairs, multiplied repeatedly for ~cpu_seconds
+    cnt = 4 * share  # a fixed set of pairs, multiplied repeatedly for ~cpu_seconds
     a = np.zeros(cnt * 2 * L * n, dtype=np.uint64)
     b = np.zeros_like(a)
     out = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
     ora.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 11)
     ora.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 12)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        ora.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk))
-        done += cnt
-        dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds:
-            break
+    legs = {}
+    for threads in (share, 4):
+        gomp.omp_set_num_threads(threads)
+        batch = max(threads, 4)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            ora.lib.he_mul_rescale_batch(out.ctypes.data, a.ctypes.data, b.ctypes.data, batch, L, ctypes.byref(rlk))
+            done += batch
+            dt = time.perf_counter() - t0
+            if dt >= args.cpu_seconds:
+                break
+        legs[threads] = (done / dt, done, dt)
     ora.exit()
-    cnt = done
-    return {"value": cnt / dt, "unit": "ct-mult/s", "cores": threads, "kind": "port",
-            "sample": f"{cnt} ct x ct+relin+rescale ops at N=2^{logn}, L={L}, dnum={dnum} "
-                      f"({4 * threads} distinct pairs, OpenMP over the batch, {dt:.1f} s)"}
+    v, done, dt = legs[share]
+    v4, done4, dt4 = legs[4]
+    return {"value": v, "unit": "ct-mult/s", "cores": share, "kind": "port",
+            "sample": f"{done} ct x ct+relin+rescale ops at N=2^{logn}, L={L}, dnum={dnum} on {share} threads "
+                      f"(OpenMP over batches of {max(share, 4)} distinct pairs, {dt:.1f} s)",
+            "threads_4": {"value": v4, "cores": 4, "sample": f"{done4} ops, batches of 4, {dt4:.1f} s"},
+            "host_cpus_usable": usable_cpus(), "host_cpus_total": os.cpu_count(),
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "note": "threads = OMP_NUM_THREADS (this job's CPU share on the GPU box), not every visible CPU"}
+
+
+# ---------------------------------------------------------------------------
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.launch_check:
+        return launch_check(args)
+    import torch
+    import torch.distributed as dist
+
+    from hectr_amd import dist as hdist
+
+    rank, world, local = hdist.env()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # one process per GPU; the modulus only matters for rehearsals with more
+    # ranks than GPUs (HECTR_DIST_BACKEND=gloo: RCCL needs distinct devices)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    backend = os.environ.get("HECTR_DIST_BACKEND", "nccl")
+    hdist.init(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    barrier = hdist.barrier
+
+    L, logn, B = args.nlimbs, args.logn, args.batch
+    dnum = args.dnum or L
+    stream = torch.cuda.Stream()
+    mb = MulBatch(stream, logn, L, dnum, args.q0_bits, args.p_bits, args.nspecial, B, rank * B, 1000 + rank)
+    eng = mb.eng
+    elapsed = timed(mb.step, args.steps, args.warmup, eng.sync, barrier)
+    elapsed = hdist.max_over_ranks(elapsed, device=red_dev)
+    value = world * B * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # instrumented pass (same steps): per-kernel device time from HIP events on
+    # the engine stream, streamed bytes per launch from the library
+    eng.prof_enable(True)
+    ti0 = time.perf_counter()
+    for _ in range(args.steps):
+        mb.step()
+    eng.sync()
+    ti1 = time.perf_counter()
+    stats = eng.prof_collect()
+    eng.prof_enable(False)
+    step_s = (ti1 - ti0) / args.steps
+    launches_per_step = stats[max(stats, key=lambda k: stats[k][1])][0] / args.steps
+    pairs_per_launch = int(round(B / launches_per_step))
+    workload = (f"ct x ct mult + relin + rescale, N=2^{logn}, L={L}, K={mb.K}, dnum={mb.dnum}, "
+                f"primes {args.q0_bits}/50/{args.p_bits} bits, batch={B} pairs per GPU")
+
+    result = None
+    if rank == 0:
+        kernels = {k: {"launches": v[0], "avg_us": v[1] / v[0], "share": v[1] / (1e6 * step_s * args.steps),
+                       "streamed_GBs": v[2] / v[1] / 1e3} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
+        alg = mb.alg_bytes()
+        result = {
+            "metric": "ct×ct+relin/sec at N=2^16, L=8 RNS primes; encrypted CSTR-MPC steps/sec",
+            "value": value,
+            "unit": "ct-mult/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic random-residue ciphertexts (splitmix64), real relinearization key",
+            "config": {"workload": workload,
+                       "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": mb.K,
+                       "dnum": mb.dnum, "prime_bits": {"q0": args.q0_bits, "qi": 50, "p": args.p_bits},
+                       "pairs_per_launch": pairs_per_launch,
+                       "parallelism": f"batch-sharded x{world}"},
+            "per_gpu_value": value / world,
+            "op_roofline": {"alg_bytes_per_op": alg, "achieved_GBs": alg * value / world / 1e9,
+                            "frac": alg * value / world / 1e9 / HBM_PEAK_GBS},
+            "roofline": roofline(stats, step_s * args.steps, mb, workload, pairs_per_launch),
+            "kernels": kernels,
+            "instrumented_ms_per_step": 1e3 * step_s,
+        }
+        if world == 1 and not args.no_ntt:
+            result["ntt_roundtrip"] = ntt_roundtrip(eng, stream, logn, L, args.ntt_polys)
+    mb.close()
+    barrier()
+
+    if args.alt_bits and args.alt_bits != args.q0_bits:
+        # the conventional prime sizes (60-bit q0 and special primes: the
+        # integer butterflies on those limbs), same op, batch and harness
+        alt = MulBatch(stream, logn, L, dnum, args.alt_bits, args.alt_bits, 0, B, rank * B, 1000 + rank)
+        t = hdist.max_over_ranks(timed(alt.step, args.steps, 1, alt.eng.sync, barrier), device=red_dev)
+        if rank == 0:
+            v = world * B * args.steps / t
+            result["value_60bit"] = v
+            result["alt_primes"] = {"q0_bits": args.alt_bits, "qi_bits": 50, "p_bits": args.alt_bits,
+                                    "nspecial": alt.K, "value": v, "unit": "ct-mult/s", "steps": args.steps,
+                                    "op_roofline_frac": alt.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
+        alt.close()
+        barrier()
+
+    if not args.no_c5:
+        # config 5: n = 2^17, L = 12 (dnum 3, K 4, conventional primes), each
+        # rank its own shard of the global batch
+        c5 = MulBatch(stream, 17, 12, 3, 60, 60, 4, args.c5_batch, rank * args.c5_batch, 2000 + rank)
+        steps5 = max(2, args.steps // 2)
+        t = hdist.max_over_ranks(timed(c5.step, steps5, 1, c5.eng.sync, barrier), device=red_dev)
+        if rank == 0:
+            v = world * args.c5_batch * steps5 / t
+            result["config5"] = {"workload": f"ct x ct mult + relin + rescale, N=2^17, L=12, K=4, dnum=3, "
+                                             f"primes 60/50/60 bits, batch={args.c5_batch} pairs per GPU",
+                                 "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "ct-mult/s",
+                                 "steps": steps5, "ms_per_step": 1e3 * t / steps5,
+                                 "op_roofline_frac": c5.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
+        c5.close()
+        barrier()
+
+    if rank == 0 and world == 1 and not args.no_cstr:
+        result["cstr"] = cstr_loop(args.cstr_steps)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, logn, L, dnum)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

@@ -396,17 +396,6 @@ extern "C" void hectx_exit(void)
   if (!G.init)
     return;
   HIP_CHECK(hipStreamSynchronize(G.stream));
-  for (int s = 0; s < 2; s++)
-    if (G.lane[s]) {
-      HIP_CHECK(hipStreamSynchronize(G.lane[s]));
-      HIP_CHECK(hipStreamDestroy(G.lane[s]));
-      G.lane[s] = nullptr;
-    }
-  for (int e = 0; e < 3; e++)
-    if (G.lane_ev[e]) {
-      HIP_CHECK(hipEventDestroy(G.lane_ev[e]));
-      G.lane_ev[e] = nullptr;
-    }
   gemv_cache_clear();
   tables_free();
   pool_release_all();
@@ -801,20 +790,11 @@ extern "C" void he_mul_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt)
   out->flags = 0;
 }
 
-// Where the fused path adds the tensor terms d0/d1 of the keep limbs: in the
-// key switch's accumulator as P (d0, d1) (default: ks_rows2's loads overlap
-// its latency-bound row passes) or in the ModDown epilogue after the division
-// (GPQHE_D01_KS=0; dn_rows is HBM-bound).  Same-box A/B at N=2^16, L=8:
-// 31.1k vs 30.1k ct-mult/s (ks_rows2 +120 us, dn_rows -215 us per chunk).
-static bool d01_in_ks()
-{
-  const char *e = getenv("GPQHE_D01_KS");
-  return !e || atoi(e);
-}
-
 // Tensor + relinearize [+ rescale] for `count` ciphertext pairs.
 //   a, b: ciphertext i at a + i*in_stride, c1 at + in_pstride;
 //   out:  polynomial p (= 2 i + {0,1}) at out + p*out_pstride.
+// out may overlap a or b (he_mul(c, c, b)): every input read precedes the
+// final ModDown kernel, the only writer of out, on one stream.
 static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
                       size_t in_pstride, unsigned count, unsigned lvl, const he_evk_t *rlk, bool rescale)
 {
@@ -822,76 +802,32 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
     gpqhe_die("relinearization key missing or built for another dnum");
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  const size_t d01_stride = 2 * lvl * n, d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n,
-               acc_stride = 2 * nm * n;
-  const bool fused = k_ks_fused_ok() && rlk->reserved && !getenv("GPQHE_UNFUSED");
-  // fused path: d0/d1 are formed by their consumers from a and b (no tensor
-  // buffer) unless GPQHE_TENSOR asks for the materialized one (A/B switch)
-  // (and only when out does not overlap an input: ModDown writes out while
-  // other blocks still read a and b)
-  const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
-  const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
-  auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
-  // (the opt-in row form writes d0/d1 from its tensor kernel: buffer needed)
-  const bool lazy = fused && !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) && !overlap(b);
-  Ws d01(lazy ? 0 : count * d01_stride), d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
-  if (fused) {
+  const size_t d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n, acc_stride = 2 * nm * n;
+  Ws d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
+  if (k_ks_fused_ok() && rlk->reserved) {
+    // fused path (2^13 <= n <= 2^17): d0/d1 are formed by the key switch from
+    // a and b (no tensor buffer); the ModDown runs on the dropped limbs'
+    // inverse row passes
     Ws y(count * d2_stride);
-    const int mode = rescale ? 1 : 0;
-    const bool dn_fused = !getenv("GPQHE_DN_UNFUSED");
     const unsigned keep = rescale ? lvl - 1 : lvl;
-    // keep slots' MAC deferred into the ModDown rows (kd_rows_kernel)
-    const bool defer = dn_fused && k_ks_defer_ok(lvl);
     const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
-    const bool dks = dn_fused && !defer && d01_in_ks();
-    const D01Src src = k_mul_keyswitch_fused(acc.p, d01.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride, evkm, count,
-                                             lvl, dn_fused && !dks ? keep : 0, dn_fused ? keep : nm, lazy,
-                                             defer ? keep : 0);
-    if (dn_fused) {
-      const KsDeferred ks{D.p, d2.p, evkm};
-      k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, mode, dks ? D01Src{} : src, nullptr,
-                      defer ? &ks : nullptr);
-      return;
-    }
-  } else {
-    k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
-    k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
-    k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
-    unsigned mods[GPQHE_MAXMOD];
-    basis_qp(lvl, mods);
-    k_ntt(limbset(D.p, mods, nm, count * ndig, nm * n), false);
-    k_ks_inner(acc.p, D.p, count, D_stride, acc_stride, rlk->data, lvl, 1, d01.p, d01.p + lvl * n, d01_stride,
-               nullptr, false);
+    k_mul_keyswitch_fused(acc.p, d2.p, y.p, D.p, a, b, in_stride, in_pstride, evkm, count, lvl, keep);
+    k_moddown_fused(out, out_pstride, acc.p, nm * n, 2 * count, lvl, rescale ? 1 : 0);
+    return;
   }
+  // generic path (n <= 2^12: HECTR's own ring): materialized tensor, ModUp,
+  // NTT, inner product, ModDown as separate launches
+  const size_t d01_stride = 2 * lvl * n;
+  Ws d01(count * d01_stride);
+  k_tensor(d01.p, d2.p, a, b, lvl, in_stride, in_pstride, count, d01_stride);
+  k_ntt(qlimbs(d2.p, lvl, count, d2_stride), true);
+  k_modup(D.p, d2.p, count, d2_stride, D_stride, lvl);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  k_ntt(limbset(D.p, mods, nm, count * ndig, nm * n), false);
+  k_ks_inner(acc.p, D.p, count, D_stride, acc_stride, rlk->data, lvl, 1, d01.p, d01.p + lvl * n, d01_stride,
+             nullptr, false);
   k_moddown(out, out_pstride, acc.p, nm * n, 2 * count, lvl, rescale ? 1 : 0);
-}
-
-// Workspace of one pipeline lane of he_mul_rescale_batch (fused path).
-struct LaneWs {
-  uint64_t *d01, *d2, *y, *T1, *acc, *conv;
-};
-
-// mul_chunk's fused path on caller-owned workspace (no pool traffic, so it
-// may run on any stream).
-static void mul_chunk_fused(const LaneWs &w, uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
-                            size_t in_stride, size_t in_pstride, unsigned count, unsigned lvl, const he_evk_t *rlk,
-                            bool rescale)
-{
-  const unsigned nm = lvl + G.K, keep = rescale ? lvl - 1 : lvl;
-  const size_t n = G.n;
-  const size_t out_words = (2 * (size_t)count - 1) * out_pstride + (size_t)lvl * n;
-  const size_t in_words = ((size_t)count - 1) * in_stride + in_pstride + (size_t)lvl * n;
-  auto overlap = [&](const uint64_t *x) { return out < x + in_words && x < out + out_words; };
-  const bool defer = k_ks_defer_ok(lvl), dks = !defer && d01_in_ks();
-  const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
-  const D01Src src = k_mul_keyswitch_fused(w.acc, w.d01, w.d2, w.y, w.T1, a, b, in_stride, in_pstride, evkm, count,
-                                           lvl, dks ? 0 : keep, keep,
-                                           !getenv("GPQHE_TENSOR") && !getenv("GPQHE_KS_ROWFORM") && !overlap(a) &&
-                                               !overlap(b),
-                                           defer ? keep : 0);
-  const KsDeferred ks{w.T1, w.d2, evkm};
-  k_moddown_fused(out, out_pstride, w.acc, nm * n, 2 * count, lvl, rescale ? 1 : 0, dks ? D01Src{} : src, w.conv,
-                  defer ? &ks : nullptr);
 }
 
 static void mul_core(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, const he_evk_t *rlk, bool rescale)
@@ -1042,9 +978,6 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     started = true;
     dg.count = 0;
   };
-  const bool batched = !getenv("GPQHE_GEMV_PER_DIAG");
-  if (!batched)
-    HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   for (unsigned d = 0; d < s; d++) {
     bool nz = false;
     for (unsigned i = 0; i < s; i++) {
@@ -1055,29 +988,20 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     }
     if (!nz)
       continue;
-    if (batched && diag_cache_full(lvl))
+    if (diag_cache_full(lvl))
       flush();  // the cache may be cleared below: launch what refers to it first
     const uint64_t *pt = diag_pt(diag.data(), s, lvl);
     const uint64_t g = d == 0 ? 1 : galois_of_rot(d);
     const he_evk_t *k = d == 0 ? nullptr : find_rot_key(rk, d, g);
-    if (batched) {
-      dg.evk[dg.count] = k ? k->data : nullptr;
-      dg.pt[dg.count] = pt;
-      dg.g[dg.count] = g;
-      if (++dg.count == GemvDiags::MAX)
-        flush();
-      continue;
-    }
-    if (d == 0)
-      k_ks_inner(acc.p, D.p, 1, 0, 0, nullptr, lvl, 1, limb(x, 0, 0), limb(x, 1, 0), 0, pt, true);
-    else
-      k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(x, 0, 0), nullptr, 0, pt, true);
+    dg.evk[dg.count] = k ? k->data : nullptr;
+    dg.pt[dg.count] = pt;
+    dg.g[dg.count] = g;
+    if (++dg.count == GemvDiags::MAX)
+      flush();
   }
-  if (batched) {
-    flush();
-    if (!started)  // all-zero matrix
-      HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
-  }
+  flush();
+  if (!started)  // all-zero matrix
+    HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   const double scale = x->scale;
   k_moddown(y->data, pstride(y), acc.p, nm * n, 2, lvl, 1);
   y->nlimbs = lvl - 1;
@@ -1107,68 +1031,18 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   static const size_t budget = (size_t)env_u("GPQHE_WS_MIB", 8192) << 20;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));
-  if (const char *e = getenv("GPQHE_CHUNK"))  // test hook: force small chunks (several lanes' worth)
+  if (const char *e = getenv("GPQHE_CHUNK"))  // test hook: force several chunks on a small batch
     chunk = std::max<size_t>(1, std::min<size_t>(chunk, strtoul(e, nullptr, 0)));
   // equal chunks: a short last chunk runs at a fraction of the GPU's width
   const size_t nchunks = (count + chunk - 1) / chunk;
   if (nchunks)
     chunk = (count + nchunks - 1) / nchunks;
   const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
-  const bool lanes = nchunks >= 2 && k_ks_fused_ok() && rlk->reserved && rlk->dnum == G.dnum &&
-                     !getenv("GPQHE_UNFUSED") && !getenv("GPQHE_DN_UNFUSED") && getenv("GPQHE_LANES") &&
-                     !k_prof_on();
-  if (!lanes) {
-    for (size_t c0 = 0; c0 < count; c0 += chunk) {
-      const unsigned cnt = (unsigned)std::min(chunk, count - c0);
-      mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n,
-                cnt, lvl, rlk, true);
-    }
-    return;
-  }
-  // Two pipeline lanes (HIP streams), chunks alternating, so one chunk's
-  // memory-bound kernels could share the CUs with the other's VALU-bound ones.
-  // Opt-in (GPQHE_LANES): measured no faster than one stream at N=2^16, L=8
-  // (each kernel fills the GPU by itself).  Each lane owns its workspace for
-  // the whole call (the pool is stream-ordered).
-  const unsigned keep = lvl - 1;
-  const size_t cw = chunk * n;
-  const size_t lane_words = cw * (2 * lvl + lvl + lvl + (size_t)ndig * nm + 2 * nm + 2 * keep);
-  uint64_t *wsb[2];
-  LaneWs ws[2];
-  for (int s = 0; s < 2; s++) {
-    if (!G.lane[s])
-      HIP_CHECK(hipStreamCreateWithFlags(&G.lane[s], hipStreamNonBlocking));
-    wsb[s] = (uint64_t *)pool_alloc(lane_words * 8);
-    uint64_t *q = wsb[s];
-    ws[s].d01 = q, q += cw * 2 * lvl;
-    ws[s].d2 = q, q += cw * lvl;
-    ws[s].y = q, q += cw * lvl;
-    ws[s].T1 = q, q += cw * ndig * nm;
-    ws[s].acc = q, q += cw * 2 * nm;
-    ws[s].conv = q;
-  }
-  for (int e = 0; e < 3; e++)
-    if (!G.lane_ev[e])
-      HIP_CHECK(hipEventCreateWithFlags(&G.lane_ev[e], hipEventDisableTiming));
-  const hipStream_t main = G.stream;
-  HIP_CHECK(hipEventRecord(G.lane_ev[2], main));
-  for (int s = 0; s < 2; s++)
-    HIP_CHECK(hipStreamWaitEvent(G.lane[s], G.lane_ev[2], 0));
-  size_t i = 0;
-  for (size_t c0 = 0; c0 < count; c0 += chunk, i++) {
+  for (size_t c0 = 0; c0 < count; c0 += chunk) {
     const unsigned cnt = (unsigned)std::min(chunk, count - c0);
-    G.stream = G.lane[i & 1];
-    mul_chunk_fused(ws[i & 1], out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride,
-                    in_stride, lvl * n, cnt, lvl, rlk, true);
+    mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n, cnt,
+              lvl, rlk, true);
   }
-  G.stream = main;
-  for (int s = 0; s < 2; s++) {
-    HIP_CHECK(hipEventRecord(G.lane_ev[s], G.lane[s]));
-    HIP_CHECK(hipStreamWaitEvent(main, G.lane_ev[s], 0));
-  }
-  // freed in main-stream order: later work on main runs after both lanes
-  pool_free(wsb[0]);
-  pool_free(wsb[1]);
 }
 
 static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)

@@ -205,8 +205,6 @@ struct Context {
   const double *twd = nullptr, *itwd = nullptr;    // interleaved (w, w / q) doubles [nmod][n][2]
   hipStream_t stream = nullptr;
   hipStream_t own_stream = nullptr;
-  hipStream_t lane[2] = {nullptr, nullptr};  // he_mul_rescale_batch pipeline lanes
-  hipEvent_t lane_ev[3] = {nullptr, nullptr, nullptr};
   int device = 0;
 };
 
@@ -284,44 +282,27 @@ void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t see
 void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 bool k_ks_fused_ok();
-// Where the tensor terms d0 = a0 b0 (poly 2 i) and d1 = a0 b1 + a1 b0 (poly
-// 2 i + 1) of ciphertext pair i come from: a materialized buffer (d01 poly P
-// at d01 + P * pstride), or -- d01 == nullptr -- the input pairs themselves
-// (a, b: pair i at + i * in_stride, c1 at + in_pstride), the products formed
-// by each consumer as it reads them.  Limb t word k of a poly sits at
-// (t << logn) + k in both.
+// The tensor terms d0 = a0 b0 (poly 2 i) and d1 = a0 b1 + a1 b0 (poly 2 i + 1)
+// of ciphertext pair i are never materialized: the key switch forms them from
+// the input pairs (pair i at a / b + i * in_stride, c1 at + in_pstride; limb t
+// word k at (t << logn) + k) and adds P (d0, d1) to its accumulators.
 struct D01Src {
-  const uint64_t *d01;
-  size_t pstride;
   const uint64_t *a, *b;
   size_t in_stride, in_pstride;
 };
-// Tensor product of `count` pairs (a, b: pair i at + i*in_stride, c1 at +
-// in_pstride) + fused relinearization.  p_lo: P (d0, d1) is added to acc
-// limbs t in [p_lo, lvl) only; the fused ModDown adds the remaining d0/d1
-// terms after its division.  Limbs t >= drop_lo leave after the inverse row
-// pass (input of k_moddown_fused).  lazy: d0/d1 are never materialized (d01
-// unused; d2 comes from a fused product + inverse row pass); returns the
-// D01Src that k_moddown_fused must read.  t_lo > 0 (k_ks_defer_ok): acc slots
-// below t_lo are not computed (k_moddown_fused's KsDeferred does them).
-D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
-                             const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
-                             const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
-                             bool lazy, unsigned t_lo = 0);
-// Inputs of the key-switch slots that k_mul_keyswitch_fused left to the
-// ModDown (t_lo = keep): T1 and the NTT-form d2 of the same call, the
-// Montgomery-form key.  Strides as k_mul_keyswitch_fused's workspaces.
-struct KsDeferred {
-  const uint64_t *T1, *d2, *evkm;
-};
-bool k_ks_defer_ok(unsigned lvl);
-// ModDown (mode 0 or 1) of X fused with the d0/d1 terms left out by
-// k_keyswitch_fused(p_lo = drop_lo = mode ? lvl - 1 : lvl): X's drop limbs
-// must hold the inverse row pass of their NTT form.  ks != nullptr: X's keep
-// limbs were not computed (t_lo = keep); their MAC runs here from ks.
+// d2 = a1 b1 of `count` pairs -> INTT -> ModUp -> key inner product + P (d0,
+// d1) into acc [count][2][lvl + K] (NTT domain).  Limbs t >= drop_lo leave after
+// the inverse row pass (the input k_moddown_fused expects).  d2 [count][lvl],
+// ybuf [count][lvl] and T1 [count][ndig][lvl + K] are workspaces.  Every read
+// of a and b happens here, so the ModDown may write over them (in place).
+D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d2, uint64_t *ybuf, uint64_t *T1, const uint64_t *a,
+                             const uint64_t *b, size_t in_stride, size_t in_pstride, const uint64_t *evkm,
+                             unsigned count, unsigned lvl, unsigned drop_lo);
+// ModDown (mode 0: / P, 1: / P q_{lvl-1}) of X whose drop limbs hold the
+// inverse row pass of their NTT form (k_mul_keyswitch_fused with drop_lo =
+// keep).
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode, const D01Src &d01, uint64_t *conv_ws = nullptr,
-                     const KsDeferred *ks = nullptr);
+                     unsigned lvl, int mode);
 bool k_prof_on();
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();

@@ -39,20 +39,18 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 // around each launch on the engine stream.
 // ===========================================================================
 enum KClass {
-  KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_NTT_COLS_FWD, KC_NTT_ROWS_FWD, KC_NTT_ROWS_INV, KC_NTT_COLS_INV,
-  KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS, KC_KS_ROWS, KC_MONT, KC_DN_COLS,
-  KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV, KC_NTT2_COLS_INV, KC_NTT2_ROWS_FWD,
-  KC_NTT2_ROWS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KD_ROWS, KC_COUNT
+  KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
+  KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
+  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
 static const char *kc_names[KC_COUNT] = {
-  "ntt_whole_kernel<fwd>", "ntt_whole_kernel<inv>", "ntt_cols_kernel<fwd>", "ntt_rows_kernel<fwd>",
-  "ntt_rows_kernel<inv>", "ntt_cols_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
-  "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "to_mont_kernel", "dn_cols_kernel",
-  "dn_rows_kernel", "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
-  "ntt2_cols_kernel<inv>", "ntt2_rows_kernel<fwd>", "ntt2_rows_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel",
-  "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>", "gemv_inner_kernel", "kd_rows_kernel"};
+  "ntt_whole_kernel<fwd>", "ntt_whole_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
+  "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "dn_cols_kernel", "dn_rows_kernel",
+  "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
+  "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
+  "gemv_inner_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -325,77 +323,6 @@ __global__ void __launch_bounds__(TPB) ntt_whole_kernel(LimbSet s, unsigned logn
   }
 }
 
-// Column pass of n = n1 x n2: tile = n1 rows x COLS columns.
-// grid.x = n2 / COLS, grid.y = limb.
-#define COLS 16
-template <bool inverse>
-__global__ void __launch_bounds__(TPB) ntt_cols_kernel(LimbSet s, unsigned logn, unsigned logn1, DevTables t)
-{
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  const unsigned logn2 = logn - logn1;
-  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
-  const unsigned v = blockIdx.y;
-  uint64_t *x = s.limb(v, logn);
-  const unsigned m = s.mod(v);
-  const ModConst mc = t.mc[m];
-  const unsigned col0 = blockIdx.x * COLS;
-  constexpr int ES = COLS + 1;
-  for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
-    const unsigned r = e / COLS, c = e % COLS;
-    lds[r * ES + c] = x[(size_t)r * n2 + col0 + c];
-  }
-  __syncthreads();
-  if constexpr (!inverse) {
-    tile_fwd<false>(lds, COLS, logn1, 1, ES, n1, 0, t.tw + ((size_t)m << logn), t.twp + ((size_t)m << logn),
-                    mc.q);
-    for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
-      const unsigned r = e / COLS, c = e % COLS;
-      x[(size_t)r * n2 + col0 + c] = lds[r * ES + c];
-    }
-  } else {
-    tile_inv<false>(lds, COLS, logn1, 1, ES, n1, 0, t.itw + ((size_t)m << logn), t.itwp + ((size_t)m << logn),
-                    mc.q);
-    for (unsigned e = threadIdx.x; e < n1 * COLS; e += blockDim.x) {
-      const unsigned r = e / COLS, c = e % COLS;
-      x[(size_t)r * n2 + col0 + c] = mul_shoup(lds[r * ES + c], mc.ninv, mc.ninvp, mc.q);
-    }
-  }
-}
-
-// Row pass: tile = ROWS rows x n2 columns; grid.x = n1 / ROWS.
-template <bool inverse>
-__global__ void __launch_bounds__(TPB) ntt_rows_kernel(LimbSet s, unsigned logn, unsigned logn1, unsigned rows,
-                                                        DevTables t)
-{
-  extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-  const unsigned logn2 = logn - logn1;
-  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
-  const unsigned v = blockIdx.y;
-  uint64_t *x = s.limb(v, logn);
-  const unsigned m = s.mod(v);
-  const ModConst mc = t.mc[m];
-  const unsigned row0 = blockIdx.x * rows;
-  const int SS = n2 + 1;
-  uint64_t *xt = x + (size_t)row0 * n2;
-  for (unsigned e = threadIdx.x; e < rows * n2; e += blockDim.x) {
-    const unsigned r = e >> logn2, c = e & (n2 - 1);
-    lds[r * SS + c] = xt[e];
-  }
-  __syncthreads();
-  const uint64_t base0 = ((uint64_t)n1 + row0) << logn2;
-  if constexpr (!inverse)
-    tile_fwd<true>(lds, rows, logn2, SS, 1, base0, n2, t.tw + ((size_t)m << logn), t.twp + ((size_t)m << logn),
-                   mc.q);
-  else
-    tile_inv<true>(lds, rows, logn2, SS, 1, base0, n2, t.itw + ((size_t)m << logn),
-                   t.itwp + ((size_t)m << logn), mc.q);
-  for (unsigned e = threadIdx.x; e < rows * n2; e += blockDim.x) {
-    const unsigned r = e >> logn2, c = e & (n2 - 1);
-    xt[e] = lds[r * SS + c];
-  }
-}
-
-
 // ===========================================================================
 // NTT v2 (two-pass, n = 2^13 .. 2^16): 4096-element tiles, 256 threads,
 // Harvey lazy butterflies (values in [0, 4q) inside a pass, canonical at every
@@ -621,12 +548,6 @@ __device__ __forceinline__ double fbc_term(double y, double c, double cq, double
 
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
 
-// Debug ablation mask for timing studies of ks_rows2 (GPQHE_ABLATE; results
-// are wrong when set): 1 skip row NTT, 2 skip key MAC, 4 skip acc stores, 8
-// skip the inverse row pass.  (dn_cols / ks_cols4 were studied the same way;
-// DESIGN.md 5 records the split.)
-static const int g_ablate = getenv("GPQHE_ABLATE") ? atoi(getenv("GPQHE_ABLATE")) : 0;
-
 // Run f with the arithmetic policy of modulus index m (q = its prime).
 template <class F>
 __device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
@@ -638,15 +559,12 @@ __device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn
     f(ArInt{q, tw.fwd + o, tw.inv + o});
 }
 
-// FP64 basis conversion per kernel (GPQHE_FBC64 bit mask, timing studies):
-// 1 ks_cols4 with the INVC column pass, 2 dn_cols, 4 ks_cols4 NT = 4.  All are
-// exact; the mask only selects the faster form (same box: INVC ks_cols4 323 vs
-// 388 us per chunk with FP64; NT = 4 ks_cols4 488 vs 308 us with FP64).
-static int fbc64_mask()
-{
-  static const int m = getenv("GPQHE_FBC64") ? atoi(getenv("GPQHE_FBC64")) : 3;
-  return m;
-}
+// FP64 basis conversion (fbc_term) where it measured faster than the 128-bit
+// integer sums + REDC (same box, per 64-pair chunk at N=2^16, L=8): the INVC
+// ks_cols4 (323 vs 388 us) and dn_cols (296 vs 309 us).  The NT = 4 ks_cols4
+// (config 5) keeps the integer sums (308 vs 488 us with FP64).  Both forms are
+// exact, so the choice never changes a bit.
+constexpr bool FBC64_KS_INVC = true, FBC64_DN = true, FBC64_KS_NT4 = false;
 
 // with_arith for kernels instantiated per prime set: ALL_F64 (every modulus
 // < 2^51, FP64 tables present) keeps only the FP64 policy in the code.
@@ -768,90 +686,6 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, un
     swp = post ? post[2 * (v % s.per) + 1] : mc.ninvp;
   }
   with_arith(mc.q, m, logn, tw, [&](const auto &ar) { cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp); });
-}
-
-// Row pass: tile = R rows x N2 columns (R N2 = 4096).
-template <int LOGN2, bool INV>
-__global__ void __launch_bounds__(256) ntt2_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
-                                                         const ModConst *mcs)
-{
-  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
-  const unsigned n1 = 1u << (logn - LOGN2);
-  unsigned v, tile;
-  pm_decode(s, n1 / R, v, tile);
-  const unsigned m = s.mod(v);
-  const ModConst mc = mcs[m];
-  const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * R;
-  const uint64_t *x = s.limb(v, logn) + ((size_t)row0 << LOGN2);
-  uint64_t *y = o.limb(v, logn) + ((size_t)row0 << LOGN2);
-  const int t = threadIdx.x;
-  if constexpr (!INV) {
-    const uint64_t *tw2 = tw.fwd + ((size_t)m << (logn + 1));
-#pragma unroll
-    for (int it = 0; it < R / 16; it++) {
-      const int item = t + 256 * it, l = item % 16, rr = item / 16;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = x[(rr << LOGN2) + l + 16 * k];
-      fwd_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, LOGN2 - 1, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        lds[rr * SP + rswz(l + 16 * k)] = r[k];
-    }
-    __syncthreads();
-    {
-      const int g = t % (N2 / 16), rr = t / (N2 / 16);
-      uint64_t r[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = lds[rr * SP + rswz(16 * g + k)];
-      fwd_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 3, q);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        lds[rr * SP + rswz(16 * g + k)] = canon4(r[k], q, q2);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int e = t + 256 * i;
-      y[e] = lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))];
-    }
-  } else {
-    const uint64_t *tw2 = tw.inv + ((size_t)m << (logn + 1));
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int e = t + 256 * i;
-      lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = x[e];
-    }
-    __syncthreads();
-    {
-      const int g = t % (N2 / 16), rr = t / (N2 / 16);
-      uint64_t r[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = lds[rr * SP + rswz(16 * g + k)];
-      inv_stages<4>(r, tw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        lds[rr * SP + rswz(16 * g + k)] = r[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < R / 16; it++) {
-      const int item = t + 256 * it, l = item % 16, rr = item / 16;
-      uint64_t r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = lds[rr * SP + rswz(l + 16 * k)];
-      inv_stages<LEA>(r, tw2, (uint64_t)(n1 + row0 + rr) << LOGN2, 4, q);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        y[(rr << LOGN2) + l + 16 * k] = canon4(r[k], q, q2);
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1135,30 +969,20 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const unsigned blocks = s.count * (n / 4096);
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const double pass_bytes = 16.0 * n * s.count;
-  static const bool rows8_env = !getenv("GPQHE_NTT2ROWS");
-  const bool rows8 = rows8_env || LOGN2 > 8;  // the 16-element row kernels need 4096 / N2 >= 16 rows
   if (!inverse) {
     {
       ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
       hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
                          G.dev.mc, (const uint64_t *)nullptr);
     }
-    ProfScope ps(rows8 ? KC_NTT3_ROWS_FWD : KC_NTT2_ROWS_FWD, pass_bytes);
-    if (rows8)
-      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
-                         G.dev.mc);
-    else if constexpr (LOGN2 <= 8)
-      hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, false>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
-                         G.dev.mc);
+    ProfScope ps(KC_NTT3_ROWS_FWD, pass_bytes);
+    hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
+                       G.dev.mc);
   } else {
     {
-      ProfScope ps(rows8 ? KC_NTT3_ROWS_INV : KC_NTT2_ROWS_INV, pass_bytes);
-      if (rows8)
-        hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn,
-                           tw, G.dev.mc);
-      else if constexpr (LOGN2 <= 8)
-        hipLaunchKernelGGL((ntt2_rows_kernel<LOGN2, true>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
-                           G.dev.mc);
+      ProfScope ps(KC_NTT3_ROWS_INV, pass_bytes);
+      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn, tw,
+                         G.dev.mc);
     }
     ProfScope ps(KC_NTT2_COLS_INV, pass_bytes);
     hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
@@ -1167,10 +991,10 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   HIP_CHECK(hipGetLastError());
 }
 
-// v2 path available for this ring degree?
+// two-pass path for this ring degree?
 static bool ntt2_ok()
 {
-  return G.logn >= 13 && G.logn <= 17 && !getenv("GPQHE_NTT_V1");
+  return G.logn >= 13 && G.logn <= 17;
 }
 
 // Out-of-place NTT (in and out have the same geometry; out may equal in);
@@ -1315,7 +1139,7 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
 // forward NTT (one launch for n <= 2^12).
 void k_lift_ntt(const LimbSet &s, const int64_t *coef)
 {
-  if (G.logn >= 10 && G.logn <= 12 && !getenv("GPQHE_NTT_WHOLE_V1")) {
+  if (G.logn >= 10 && G.logn <= 12) {
     ProfScope ps(KC_NTT_SMALL_FWD, 8.0 * G.n * (s.count + 1));
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern, unsigned threads) {
@@ -1341,7 +1165,7 @@ void k_ntt(const LimbSet &s, bool inverse)
   const unsigned logn = G.logn, n = G.n;
   if (s.count > 65535)
     gpqhe_die("k_ntt: %u limbs in one launch", s.count);
-  if (logn >= 10 && logn <= 12 && !getenv("GPQHE_NTT_WHOLE_V1")) {
+  if (logn >= 10 && logn <= 12) {
     ProfScope ps(inverse ? KC_NTT_SMALL_INV : KC_NTT_SMALL_FWD, 16.0 * n * s.count);
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern, unsigned threads) {
@@ -1365,36 +1189,9 @@ void k_ntt(const LimbSet &s, bool inverse)
     HIP_CHECK(hipGetLastError());
     return;
   }
-  if (ntt2_ok()) {
-    k_ntt_ex(s, s, inverse, nullptr);
-    return;
-  }
-  const unsigned logn1 = logn / 2;  // 13:6x7 14:7x7 15:7x8 16:8x8 17:8x9
-  const unsigned logn2 = logn - logn1;
-  const unsigned n1 = 1u << logn1, n2 = 1u << logn2;
-  const unsigned rows = n2 >= 512 ? 8 : 16;
-  const size_t lds_cols = (size_t)n1 * (COLS + 1) * 8, lds_rows = (size_t)rows * (n2 + 1) * 8;
-  const double pass_bytes = 16.0 * n * s.count;  // each pass reads + writes every limb once
-  if (!inverse) {
-    {
-      ProfScope ps(KC_NTT_COLS_FWD, pass_bytes);
-      hipLaunchKernelGGL(ntt_cols_kernel<false>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s,
-                         logn, logn1, G.dev);
-    }
-    ProfScope ps(KC_NTT_ROWS_FWD, pass_bytes);
-    hipLaunchKernelGGL(ntt_rows_kernel<false>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
-                       logn1, rows, G.dev);
-  } else {
-    {
-      ProfScope ps(KC_NTT_ROWS_INV, pass_bytes);
-      hipLaunchKernelGGL(ntt_rows_kernel<true>, dim3(n1 / rows, s.count), dim3(TPB), lds_rows, G.stream, s, logn,
-                         logn1, rows, G.dev);
-    }
-    ProfScope ps(KC_NTT_COLS_INV, pass_bytes);
-    hipLaunchKernelGGL(ntt_cols_kernel<true>, dim3(n2 / COLS, s.count), dim3(TPB), lds_cols, G.stream, s, logn,
-                       logn1, G.dev);
-  }
-  HIP_CHECK(hipGetLastError());
+  if (!ntt2_ok())
+    gpqhe_die("k_ntt: ring degree 2^%u not supported", logn);
+  k_ntt_ex(s, s, inverse, nullptr);
 }
 
 // ===========================================================================
@@ -1454,13 +1251,6 @@ __device__ __forceinline__ uint64_t mulmod_vv(uint64_t a, uint64_t b, const ModC
 __device__ __forceinline__ void d01_fetch8(const D01Src &s, unsigned P, size_t off, const int (&pos)[8],
                                            const ModConst &m, uint64_t (&v)[8])
 {
-  if (s.d01) {
-    const uint64_t *d = s.d01 + P * s.pstride + off;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      v[k] = d[pos[k]];
-    return;
-  }
   const uint64_t *pa = s.a + (P >> 1) * s.in_stride + off, *pb = s.b + (P >> 1) * s.in_stride + off;
   if (!(P & 1)) {
 #pragma unroll
@@ -1504,10 +1294,7 @@ __device__ __forceinline__ void d01_fold_f64(const D01Src &s, unsigned i, size_t
     }
   };
   double d0[8], d1[8];
-  if (s.d01) {
-    ld8(s.d01 + (2 * i) * s.pstride + off, d0);
-    ld8(s.d01 + (2 * i + 1) * s.pstride + off, d1);
-  } else {
+  {
     double a0[8], a1[8], b0[8], b1[8];
     const uint64_t *pa = s.a + i * s.in_stride + off, *pb = s.b + i * s.in_stride + off;
     ld8(pa, a0);
@@ -2010,8 +1797,6 @@ struct UpTable {
   UpDigit *dig;   // [ndig]
   uint64_t *c;    // [ndig][8][nm]  [Qj/q_i]_t 2^64 mod q_t (Montgomery form)
   uint64_t *ysc;  // [lvl][2]       n^-1 [(Qj/q_i)^-1]_{q_i} + Shoup (folded into the INTT)
-  uint64_t *ysc1; // [lvl][2]       n1^-1 [(Qj/q_i)^-1]_{q_i}: INTT columns after tensor_rows
-  uint64_t *n2i;  // [lvl][2]       n2^-1 mod q_i (tensor_rows output scale)
   double *cd;     // [ndig][8][nm][2] ([Qj/q_i]_t, that / q_t) as doubles (FP64 conversion)
   unsigned ndig, nm;
   int f64;        // every modulus of the basis < 2^51 (and FP64 enabled): FP64 conversion
@@ -2068,18 +1853,6 @@ static UpTable &up_table(unsigned lvl)
     ysc[2 * i] = w;
     ysc[2 * i + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[i]);
   }
-  // row-form split: tensor_rows leaves n2^-1 rows^-1(d2); the column INTT then
-  // needs n1^-1 = n^-1 n2 in place of n^-1
-  std::vector<uint64_t> ysc1(2 * (size_t)lvl), n2i(2 * (size_t)lvl);
-  const uint64_t n2 = 1ull << ks_logn2();
-  for (unsigned i = 0; i < lvl; i++) {
-    const uint64_t w = hm_mul_mod(ysc[2 * i], n2 % G.q[i], G.q[i]);
-    ysc1[2 * i] = w;
-    ysc1[2 * i + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[i]);
-    const uint64_t v = hm_inv_mod(n2, G.q[i]);
-    n2i[2 * i] = v;
-    n2i[2 * i + 1] = (uint64_t)(((unsigned __int128)v << 64) / G.q[i]);
-  }
   UpTable tab;
   tab.ndig = ndig;
   tab.nm = nm;
@@ -2090,10 +1863,6 @@ static UpTable &up_table(unsigned lvl)
   HIP_CHECK(hipMemcpy(tab.cd, cd.data(), cd.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
   HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMalloc(&tab.ysc1, ysc1.size() * 8));
-  HIP_CHECK(hipMemcpy(tab.ysc1, ysc1.data(), ysc1.size() * 8, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMalloc(&tab.n2i, n2i.size() * 8));
-  HIP_CHECK(hipMemcpy(tab.n2i, n2i.data(), n2i.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.dig, ndig * sizeof(UpDigit)));
   HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
   HIP_CHECK(hipMemcpy(tab.dig, dig.data(), ndig * sizeof(UpDigit), hipMemcpyHostToDevice));
@@ -2385,72 +2154,6 @@ __global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size
   }
 }
 
-// Tensor product fused with the inverse row pass of d2 (batched relinearize,
-// alpha <= 4): d0 = a0 b0 and d1 = a0 b1 + a1 b0 are stored as they are (NTT
-// domain); d2 = a1 b1 leaves as n2^-1 rows^-1(d2).  That is exactly the column
-// intermediate of the 4-step NTT: the forward row pass of it reproduces d2
-// (ks_rows uses it as the digit's own limb), and the inverse column pass with
-// n1^-1 completes the INTT (ks_cols4 loader).
-template <int LOGN2>
-__global__ void __launch_bounds__(256) tensor_rows_kernel(uint64_t *d01, size_t d01_stride, uint64_t *d2r,
-                                                           size_t d2_stride, const uint64_t *a, const uint64_t *b,
-                                                           size_t in_stride, size_t in_pstride, unsigned logn,
-                                                           unsigned lvl, unsigned count, const uint64_t *n2i, Tw2 tw,
-                                                           const ModConst *mcs)
-{
-  constexpr int N2 = 1 << LOGN2, R = 4096 / N2, LEA = LOGN2 - 4, EA = 1 << LEA, SP = N2 + 1;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[R * SP];
-  const unsigned n1 = 1u << (logn - LOGN2);
-  const unsigned tiles = n1 / R;
-  // limb-major block order: one modulus' twiddles stay hot in L2
-  const unsigned blk = blockIdx.x, limb = blk / (count * tiles), rem = blk % (count * tiles);
-  const unsigned p = rem / tiles, tile = rem % tiles;
-  const ModConst mc = mcs[limb];
-  const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * R;
-  const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
-  const uint64_t *pa = a + p * in_stride + off, *pb = b + p * in_stride + off;
-  uint64_t *o0 = d01 + p * d01_stride + off, *o1 = o0 + ((size_t)lvl << logn);
-  const int th = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int e = th + 256 * i;
-    const uint64_t a0 = pa[e], a1 = pa[in_pstride + e], b0 = pb[e], b1 = pb[in_pstride + e];
-    o0[e] = mul_mod(a0, b0, mc);
-    o1[e] = add_mod(mul_mod(a0, b1, mc), mul_mod(a1, b0, mc), q);
-    lds[(e >> LOGN2) * SP + rswz(e & (N2 - 1))] = mul_mod(a1, b1, mc);
-  }
-  __syncthreads();
-  const uint64_t *itw2 = tw.inv + ((size_t)limb << (logn + 1));
-  {
-    const int g = th % (N2 / 16), rr = th / (N2 / 16);
-    uint64_t r[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = lds[rr * SP + rswz(16 * g + k)];
-    inv_stages<4>(r, itw2, ((uint64_t)(n1 + row0 + rr) << LOGN2) + 16 * g, 0, q);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      lds[rr * SP + rswz(16 * g + k)] = r[k];
-  }
-  __syncthreads();
-  const uint64_t w = n2i[2 * limb], wp = n2i[2 * limb + 1];
-  uint64_t *y = d2r + p * d2_stride + off;
-#pragma unroll
-  for (int it = 0; it < R / 16; it++) {
-    const int item = th + 256 * it, l = item % 16, rr = item / 16;
-    uint64_t r[EA];
-#pragma unroll
-    for (int k = 0; k < EA; k++)
-      r[k] = lds[rr * SP + rswz(l + 16 * k)];
-    inv_stages<LEA>(r, itw2, (uint64_t)(n1 + row0 + rr) << LOGN2, 4, q);
-#pragma unroll
-    for (int k = 0; k < EA; k++)
-      y[(rr << LOGN2) + l + 16 * k] = mul_shoup(r[k], w, wp, q);
-  }
-  (void)q2;
-}
-
 // Multi-target variant for digits of at most 4 limbs: the block loads its
 // (p, j, tile) digit values into registers once and converts them for NT
 // targets in turn (the single-target kernel re-reads them through L2 for every
@@ -2492,8 +2195,8 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         }
     }
   } else {
-    // the digit arrives after the inverse row pass (tensor_rows_kernel): run
-    // the inverse column pass with n1^-1 [(Qj/q_i)^-1] here, limb by limb
+    // the digit arrives after the inverse row pass (d2_rows_kernel): run the
+    // inverse column pass with n^-1 [(Qj/q_i)^-1] here, limb by limb
     auto load_limb = [&](auto I) {
       constexpr int i = decltype(I)::value;
       if (i >= (int)na) {
@@ -2505,7 +2208,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         return;
       }
       const unsigned mi_ = lo + i;
-      const uint64_t w = tab.ysc1[2 * mi_], wp = tab.ysc1[2 * mi_ + 1];
+      const uint64_t w = tab.ysc[2 * mi_], wp = tab.ysc[2 * mi_ + 1];
       const uint64_t *src = yb + ((size_t)i << logn);
       if (i)
         __syncthreads();
@@ -2629,7 +2332,7 @@ __device__ __forceinline__ unsigned own_perm(unsigned idx)
 // for (basis slot t, 2048-element row tile, ciphertext p) and each digit j,
 // the column-transformed limb T1[j][t] (own digit: the NTT-form d2 limb) gets
 // its row pass and is multiplied into the Montgomery-form key; both
-// accumulators stay in registers.  P (d0, d1) is added on [p_lo, lvl); limbs
+// accumulators stay in registers.  P (d0, d1) is added on the q limbs; limbs
 // t >= drop_lo leave after the inverse row pass (input of dn_cols).
 template <int LOGN2>
 __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
@@ -2637,7 +2340,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
                                                        const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                        unsigned nmod, unsigned ndig, unsigned alpha, unsigned count,
-                                                       unsigned p_lo, unsigned drop_lo, int own_rowform, Tw2 tw,
+                                                       unsigned drop_lo, Tw2 tw,
                                                        const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
@@ -2700,16 +2403,15 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
       const uint64_t *ea = evkm + (((size_t)(2 * j + 1) * nmod + m) << logn) + toff + th;
       V r[8];
       const bool own = t < lvl && t / alpha == j;
-      if (own && !own_rowform) {
+      if (own) {
         uint64_t v[8];
         load_own(d2n + p * d2_stride + ((size_t)t << logn) + toff, v);  // own digit: NTT-form d2
 #pragma unroll
         for (int k = 0; k < 8; k++)
           r[k] = A::load(v[k]);
       } else {
-        // converted limb from ks_cols, or (row form) the own d2 limb's column intermediate
-        const uint64_t *x = own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
-                                : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+        // converted limb from ks_cols (column pass done)
+        const uint64_t *x = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
 #pragma unroll
         for (int k = 0; k < 8; k++)
           r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
@@ -2755,7 +2457,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
       (void)f0;
       (void)f1;
     }
-    if (t < lvl && t >= p_lo) {
+    if (t < lvl) {
       // round C ownership: words 8 h + k of the thread's row
       int pos[8];
 #pragma unroll
@@ -2808,22 +2510,21 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
                                                            const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
                                                            unsigned logn, unsigned lvl, unsigned L, unsigned nm,
                                                            unsigned nmod, unsigned alpha, unsigned count,
-                                                           unsigned cpb, unsigned members, unsigned p_lo,
-                                                           unsigned drop_lo, unsigned t_lo, int own_rowform,
-                                                           Tw2 tw, const ModConst *mcs, int ablate)
+                                                           unsigned cpb, unsigned members, unsigned drop_lo,
+                                                           Tw2 tw, const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
   __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
-  unsigned grp, mi;  // group = (basis slot t >= t_lo, tile) on one XCD; members = ciphertext runs
-  if (!xcd_group(members, (nm - t_lo) * tiles, grp, mi))
+  unsigned grp, mi;  // group = (basis slot t, tile) on one XCD; members = ciphertext runs
+  if (!xcd_group(members, nm * tiles, grp, mi))
     return;
   const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
   if (p0 >= p1)
     return;
-  const unsigned t = t_lo + grp / tiles, tile = grp % tiles;
+  const unsigned t = grp / tiles, tile = grp % tiles;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
   const uint64_t q = mc.q, q2 = 2 * q;
@@ -2833,7 +2534,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
   // digit j's input for ciphertext p: own digit -> the NTT-form d2 limb
   // (natural layout, transposed through LDS), else T1[j][t] (row pass input)
   const bool own0 = t < lvl && t / alpha == 0, own1 = t < lvl && t / alpha == 1;
-  const bool nat0 = own0 && !own_rowform, nat1 = own1 && !own_rowform;
+  const bool nat0 = own0, nat1 = own1;
   auto src = [&](unsigned j, unsigned p) -> const uint64_t * {
     const bool own = j ? own1 : own0;
     return own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
@@ -2894,10 +2595,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
             r[k] = A::load(xn[j][k]);
           if (p + 1 < p1)
             fetch(xn[j], j, p + 1);
-          if (ablate & 1) {
-          } else {
-            rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
-          }
+          rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
         }
         if constexpr (std::is_same<A, ArF64>::value) {
 #pragma unroll
@@ -2916,19 +2614,14 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
             if (j == 0) {
               a0[k] = a1[k] = 0;
             }
-            if (ablate & 2) {
-              a0[k] += v;
-              a1[k] ^= v;
-            } else {
-              mac(a0[k], v, kl[2 * j][256 * k + th]);
-              mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
-            }
+            mac(a0[k], v, kl[2 * j][256 * k + th]);
+            mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
           }
         }
       }
       bool folded = false;  // P (d0, d1) added in FP64 before canonicalising
       if constexpr (std::is_same<A, ArF64>::value) {
-        if (t < lvl && t >= p_lo) {
+        if (t < lvl) {
           d01_fold_f64(d01, p, ((size_t)t << logn) + toff + 8 * th, mc, f0, f1);
           folded = true;
         }
@@ -2946,7 +2639,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
         (void)f0;
         (void)f1;
       }
-      if (!folded && t < lvl && t >= p_lo) {
+      if (!folded && t < lvl) {
         // round C ownership is natural order: words 8 th .. 8 th + 7
         int pos[8];
 #pragma unroll
@@ -2968,10 +2661,7 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
       }
       uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
       uint64_t *o1 = o0 + ((size_t)nm << logn);
-      if (ablate & 4) {
-        if (a0[0] == 0x1234567 && a1[1] == 0x89)  // keeps the values live
-          o0[th] = a0[2] + a1[3];
-      } else if (t < drop_lo || (ablate & 8)) {
+      if (t < drop_lo) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           ulonglong2 *d2 = (ulonglong2 *)((half ? o1 : o0) + 8 * th);
@@ -3003,16 +2693,12 @@ __global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, si
 
 template <int LOGT1, int LOGN2>
 static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
-                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned p_lo,
-                            unsigned drop_lo, unsigned t_lo, bool rowform, bool invc)
+                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned drop_lo,
+                            bool invc)
 {
   // invc: y holds only the inverse row pass of d2 (d2_rows_kernel, unscaled);
   // ks_cols4 runs the inverse column pass with the full n^-1 [(Qj/q_i)^-1]
-  UpTable tab = up_table(lvl);
-  if (invc && !rowform)
-    tab.ysc1 = tab.ysc;
-  rowform = rowform || invc;  // (the ks_cols4 form; ks_rows2 keeps own_rowform below)
-  const bool own_rowform = rowform && !invc;
+  const UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
   const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
                acc_stride = 2 * (size_t)nm * n;
@@ -3022,74 +2708,53 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
   {
     // reads the digit's alpha limbs once per target set (registers), writes
     // the converted + column-transformed limbs
-    ProfScope ps(rowform || G.alpha <= 4 ? KC_KS_COLS4 : KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
+    ProfScope ps(invc || G.alpha <= 4 ? KC_KS_COLS4 : KC_KS_COLS, 8.0 * n * count * ((double)lvl + ndig * nm - own));
     const unsigned ngroups = tiles * count * ndig;
-    if (rowform) {
+    const unsigned na_min = lvl - (ndig - 1) * G.alpha;
+    if (invc) {
       constexpr unsigned NT = 8;  // all targets of a digit tile: its INTT columns run once
-      const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
                            t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
       };
-      tab.f64 && (fbc64_mask() & 1) ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
-                                    : go(ks_cols4_kernel<LOGT1, NT, true, false>);
+      tab.f64 && FBC64_KS_INVC ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
+                               : go(ks_cols4_kernel<LOGT1, NT, true, false>);
     } else if (G.alpha <= 4) {
       constexpr unsigned NT = 4;
-      const unsigned na_min = lvl - (ndig - 1) * G.alpha;
       const unsigned members = (nm - na_min + NT - 1) / NT;
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
                            t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
       };
-      tab.f64 && (fbc64_mask() & 4) ? go(ks_cols4_kernel<LOGT1, NT, false, true>)
-                                    : go(ks_cols4_kernel<LOGT1, NT, false, false>);
+      tab.f64 && FBC64_KS_NT4 ? go(ks_cols4_kernel<LOGT1, NT, false, true>)
+                              : go(ks_cols4_kernel<LOGT1, NT, false, false>);
     } else {
       hipLaunchKernelGGL((ks_cols_kernel<LOGT1>), dim3(xcd_blocks(nm, ngroups)), dim3(256), 0, G.stream, y,
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
     }
   }
-  // reads T1 (+ own d2 limbs, d0/d1 on [p_lo, lvl)) per ciphertext and the key
-  // once, writes acc; slots [t_lo, nm) only (t_lo > 0: kd_rows_kernel does the
-  // lower slots inside the ModDown)
-  const bool rows2 = ndig == 2 && !getenv("GPQHE_KSROWS_STREAM");
-  if (t_lo && !rows2)
-    gpqhe_die("deferred key-switch slots need the two-digit ks_rows2 path");
-  const double ns = nm - t_lo;
+  // reads T1 (+ own d2 limbs, the four input limbs of d0/d1 on q limbs) per
+  // ciphertext and the key once, writes acc
+  const bool rows2 = ndig == 2;
   ProfScope ps(rows2 ? KC_KS_ROWS2 : KC_KS_ROWS,
-               8.0 * n * ((double)count * (ndig * ns + (d01.d01 ? 2.0 : 4.0) * (lvl - std::min(p_lo, lvl)) +
-                                           2 * ns) +
-                          2.0 * ndig * ns));
+               8.0 * n * ((double)count * (ndig * nm + 4.0 * lvl + 2 * nm) + 2.0 * ndig * nm));
   if (rows2) {
-    // key-stationary: ~4 blocks per CU over (slot, tile) groups x ciphertext runs
-    const unsigned groups = (nm - t_lo) * (n / 2048);
-    static const unsigned want = getenv("GPQHE_KSR_MEMBERS") ? atoi(getenv("GPQHE_KSR_MEMBERS")) : 0;
-    // runs of about 8 ciphertexts per block (64 pairs: 693 vs 712 us for runs
-    // of 13), more and shorter runs when the batch is too small to fill the GPU
+    // key-stationary: runs of about 8 ciphertexts per block (64 pairs: 693 vs
+    // 712 us for runs of 13), more and shorter runs when the batch is too small
+    // to fill the GPU (~6 blocks per CU over (slot, tile) groups x runs)
+    const unsigned groups = nm * (n / 2048);
     const unsigned fill = std::min(count, (6 * 256 + groups - 1) / groups);
-    const unsigned members = std::max(1u, want ? std::min(count, want) : std::max((count + 7) / 8, fill));
+    const unsigned members = std::max(1u, std::max((count + 7) / 8, fill));
     const unsigned cpb = (count + members - 1) / members;
     hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
-                       t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, G.alpha, count, cpb, members, p_lo, drop_lo, t_lo, own_rowform ? 1 : 0, tw,
-                       G.dev.mc, g_ablate);
+                       t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod, G.alpha,
+                       count, cpb, members, drop_lo, tw, G.dev.mc);
   } else {
     hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
-                       T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm,
-                       G.nmod, ndig, G.alpha, count, p_lo, drop_lo, own_rowform ? 1 : 0, tw, G.dev.mc);
+                       T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod, ndig,
+                       G.alpha, count, drop_lo, tw, G.dev.mc);
   }
-  HIP_CHECK(hipGetLastError());
-}
-
-template <int LOGN2>
-static void tensor_rows_launch(uint64_t *d01, uint64_t *d2r, const uint64_t *a, const uint64_t *b, size_t in_stride,
-                               size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab)
-{
-  ProfScope ps(KC_TENSOR, 8.0 * G.n * lvl * count * 7);  // read 4 limbs, write 3 limbs
-  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
-  hipLaunchKernelGGL((tensor_rows_kernel<LOGN2>), dim3(lvl * count * (G.n / 4096)), dim3(256), 0, G.stream, d01,
-                     (size_t)2 * lvl * G.n, d2r, (size_t)lvl * G.n, a, b, in_stride, in_pstride, G.logn, lvl, count,
-                     tab.n2i, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -3126,37 +2791,13 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   with_arith(mc.q, limb, logn, tw, [&](const auto &ar) { rows8_tile_raw<LOGN2, true>(ar, raw, yo, lds, n1 + row0); });
 }
 
-// Default on (GPQHE_KSC_INVC=0: separate ntt2_cols pass).  Same-box A/B at
-// N=2^16, L=8: 31.4k vs 30.7k ct-mult/s (ks_cols4 +80 us, ntt2_cols -128 us
-// per chunk: the column INTT is done once per digit tile, NT = 8 targets).
-static bool ks_invc()
-{
-  const char *e = getenv("GPQHE_KSC_INVC");
-  return !e || atoi(e);
-}
-
 bool k_ks_fused_ok()
 {
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
 }
 
-// The keep slots' MAC can move into the ModDown rows (kd_rows_kernel) when the
-// key has two digits (ks_rows2's key-stationary layout) and d2 stays in NTT
-// form (no row form).  Opt-in (GPQHE_KDROWS=1): it removes the keep limbs'
-// accumulator round trip (28 of ~235 limb transfers per pair at N=2^16, L=8,
-// dnum=2) but measured no faster (28.7k vs 28.6k ct-mult/s same box: the row
-// kernels are latency-bound, and kd_rows spills at 256 VGPRs).
-bool k_ks_defer_ok(unsigned lvl)
-{
-  // (read per call: the switches are per-call, as the row form's)
-  const char *e = getenv("GPQHE_KDROWS");
-  const bool on = e && atoi(e) && !getenv("GPQHE_KSROWS_STREAM") && !getenv("GPQHE_KS_ROWFORM");
-  return on && k_ks_fused_ok() && (lvl + G.alpha - 1) / G.alpha == 2;
-}
-
-// Tensor product + fused relinearization core for `count` ciphertext pairs:
-// acc [count][2][nm]; d2 [count][lvl], ybuf and T1 are workspaces, d01
-// [count][2][lvl] too unless lazy (then d0/d1 come from a and b, D01Src).
+// d2 = a1 b1 and its INTT: the inverse row pass (d2_rows_kernel), plus the
+// column pass unless ks_cols4 runs it (cols = false).
 template <int LOGT1, int LOGN2>
 static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, const uint64_t *b, size_t in_stride,
                            size_t in_pstride, unsigned count, unsigned lvl, const UpTable &tab, bool cols)
@@ -3184,62 +2825,33 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
   HIP_CHECK(hipGetLastError());
 }
 
-D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d01, uint64_t *d2, uint64_t *ybuf, uint64_t *T1,
-                             const uint64_t *a, const uint64_t *b, size_t in_stride, size_t in_pstride,
-                             const uint64_t *evkm, unsigned count, unsigned lvl, unsigned p_lo, unsigned drop_lo,
-                             bool lazy, unsigned t_lo)
+D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d2, uint64_t *ybuf, uint64_t *T1, const uint64_t *a,
+                             const uint64_t *b, size_t in_stride, size_t in_pstride, const uint64_t *evkm,
+                             unsigned count, unsigned lvl, unsigned drop_lo)
 {
-  UpTable &tab = up_table(lvl);
-  // Row form removes the d2 INTT but lengthens the (latency-bound) tensor,
-  // ks_cols and ks_rows kernels by more than it saves (20.1k vs 20.7k op/s at
-  // N=2^16, L=8); opt-in until those kernels are pipelined.
-  const bool rowform = G.alpha <= 4 && G.logn <= 16 && getenv("GPQHE_KS_ROWFORM");
-  if (rowform && lazy)
-    gpqhe_die("k_mul_keyswitch_fused: the row form needs the d01 buffer (lazy = false)");
-  if (rowform && t_lo)
-    gpqhe_die("k_mul_keyswitch_fused: deferred slots need the NTT-form d2 limbs (no row form)");
-  // invc: the d2 INTT's column pass runs inside ks_cols4 (one block per digit
-  // tile and all its targets) instead of a separate ntt2_cols pass (A/B switch)
-  // (one ks_cols4 block must own all of a digit's targets, else the column
-  // INTT repeats per block: config 5, 12 targets per digit, measured 7.6k vs
-  // 7.8k ct-mult/s, so it keeps the separate pass)
+  const UpTable &tab = up_table(lvl);
+  // invc: d2's INTT column pass runs inside ks_cols4 (one block per digit tile
+  // and all its targets: 31.4k vs 30.7k ct-mult/s at N=2^16, L=8 against a
+  // separate ntt2_cols pass).  A digit with more than 8 targets (config 5: 12)
+  // would repeat the column INTT per block (7.6k vs 7.8k), so it keeps the
+  // separate pass.
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, na_min = lvl - (ndig - 1) * G.alpha;
-  const bool invc = lazy && !rowform && G.alpha <= 4 && tab.nm - na_min <= 8 && ks_invc();
-  D01Src src{lazy ? nullptr : d01, (size_t)lvl * G.n, a, b, in_stride, in_pstride};
-  if (rowform) {
-    // d2 leaves the tensor kernel in column-intermediate form: no separate INTT
-    if (ks_logn2() == 8)
-      tensor_rows_launch<8>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
-    else
-      tensor_rows_launch<7>(d01, d2, a, b, in_stride, in_pstride, count, lvl, tab);
-  } else if (lazy) {
-    switch (G.logn) {
-    case 13: d2_intt_launch<6, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
-    case 14: d2_intt_launch<7, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
-    case 15: d2_intt_launch<7, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
-    case 16: d2_intt_launch<8, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
-    case 17: d2_intt_launch<8, 9>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
-    default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
-    }
-  } else {
-    k_tensor(d01, d2, a, b, lvl, in_stride, in_pstride, count, (size_t)2 * lvl * G.n);
-    LimbSet in{}, out{};
-    in.base = d2;
-    out.base = ybuf;
-    in.stride = out.stride = (size_t)lvl * G.n;
-    in.per = out.per = lvl;
-    in.count = out.count = lvl * count;
-    for (unsigned i = 0; i < lvl; i++)
-      in.mods[i] = out.mods[i] = (uint8_t)i;
-    k_ntt_ex(in, out, true, tab.ysc);
-  }
-  const uint64_t *y = rowform ? d2 : ybuf;
+  const bool invc = G.alpha <= 4 && tab.nm - na_min <= 8;
+  const D01Src src{a, b, in_stride, in_pstride};
   switch (G.logn) {
-  case 13: ks_fused_launch<6, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
-  case 14: ks_fused_launch<7, 7>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
-  case 15: ks_fused_launch<7, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
-  case 16: ks_fused_launch<8, 8>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
-  case 17: ks_fused_launch<8, 9>(y, T1, d2, src, evkm, acc, count, lvl, p_lo, drop_lo, t_lo, rowform, invc); break;
+  case 13: d2_intt_launch<6, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+  case 14: d2_intt_launch<7, 7>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+  case 15: d2_intt_launch<7, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+  case 16: d2_intt_launch<8, 8>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+  case 17: d2_intt_launch<8, 9>(d2, ybuf, a, b, in_stride, in_pstride, count, lvl, tab, !invc); break;
+  default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
+  }
+  switch (G.logn) {
+  case 13: ks_fused_launch<6, 7>(ybuf, T1, d2, src, evkm, acc, count, lvl, drop_lo, invc); break;
+  case 14: ks_fused_launch<7, 7>(ybuf, T1, d2, src, evkm, acc, count, lvl, drop_lo, invc); break;
+  case 15: ks_fused_launch<7, 8>(ybuf, T1, d2, src, evkm, acc, count, lvl, drop_lo, invc); break;
+  case 16: ks_fused_launch<8, 8>(ybuf, T1, d2, src, evkm, acc, count, lvl, drop_lo, invc); break;
+  case 17: ks_fused_launch<8, 9>(ybuf, T1, d2, src, evkm, acc, count, lvl, drop_lo, invc); break;
   default: gpqhe_die("fused key switching needs 2^13 <= n <= 2^17");
   }
   return src;
@@ -3276,7 +2888,6 @@ void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
 // [keep, nm)), keep basis positions [0, keep).
 struct DownTable {
   uint64_t *ysc;     // [nd][2]     n^-1 [(Dprod/d)^-1]_d + Shoup (folded into the INTT)
-  uint64_t *fin;     // [keep][2]   factor of the d0/d1 term added after division (+ Shoup)
   uint64_t *y, *yp;  // [nd]        [(Dprod/d)^-1]_d
   uint64_t *c;       // [nd][keep]  [Dprod/d]_t
   uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
@@ -3331,20 +2942,12 @@ static DownTable &down_table(unsigned lvl, int mode)
     dinv[t] = hm_inv_mod(dp, qt);
     dinvp[t] = (uint64_t)(((unsigned __int128)dinv[t] << 64) / qt);
   }
-  // fused ModDown: d0/d1 enter after division by Dprod; P Dprod^-1 is 1 (mode
-  // 0) or q_{lvl-1}^-1 (mode 1)
-  std::vector<uint64_t> ysc(2 * (size_t)nd), fin(2 * (size_t)keep);
+  std::vector<uint64_t> ysc(2 * (size_t)nd);
   for (unsigned d = 0; d < nd; d++) {
     const unsigned md = mods[keep + d];
     const uint64_t w = hm_mul_mod(G.mc[md].ninv, y[d], G.q[md]);
     ysc[2 * d] = w;
     ysc[2 * d + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[md]);
-  }
-  for (unsigned t = 0; t < keep; t++) {
-    const uint64_t qt = G.q[mods[t]];
-    const uint64_t f = mode == 1 ? hm_inv_mod(G.q[lvl - 1] % qt, qt) : 1 % qt;
-    fin[2 * t] = f;
-    fin[2 * t + 1] = (uint64_t)(((unsigned __int128)f << 64) / qt);
   }
   DownTable tab;
   tab.keep = keep;
@@ -3355,9 +2958,7 @@ static DownTable &down_table(unsigned lvl, int mode)
   HIP_CHECK(hipMalloc(&tab.cd, cd.size() * 8));
   HIP_CHECK(hipMemcpy(tab.cd, cd.data(), cd.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.ysc, ysc.size() * 8));
-  HIP_CHECK(hipMalloc(&tab.fin, fin.size() * 8));
   HIP_CHECK(hipMemcpy(tab.ysc, ysc.data(), ysc.size() * 8, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(tab.fin, fin.data(), fin.size() * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&tab.y, nd * 8));
   HIP_CHECK(hipMalloc(&tab.yp, nd * 8));
   HIP_CHECK(hipMalloc(&tab.c, c.size() * 8));
@@ -3464,7 +3065,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 //   Y    = INTT(X drop limbs) with n^-1 [(Dprod/d)^-1]_d folded into the last
 //          pass (in place)
 //   conv = forward column pass of FBC_{drop->t}(Y)      (dn_cols_kernel)
-//   out  = (X_t - NTTrows(conv_t)) Dprod^-1 + fin_t d01_t  (dn_rows_kernel)
+//   out  = (X_t - NTTrows(conv_t)) Dprod^-1              (dn_rows_kernel)
 // The converted polynomial never reaches HBM in coefficient form and the
 // combine is the row pass's epilogue.
 // ===========================================================================
@@ -3627,13 +3228,13 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 }
 
 // Forward row pass of conv on 8-element row tiles with the combine as its
-// epilogue.  The epilogue operands (X_t, d_{0,1,t}) are fetched at kernel
-// start so their latency overlaps the row pass.
+// epilogue.  The epilogue operand X_t is fetched at kernel start so its
+// latency overlaps the row pass.  (The key switch added P (d0, d1) to X.)
 template <int LOGN2>
 __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint64_t *out, size_t out_pstride,
-                                                       const uint64_t *X, size_t x_pstride, D01Src d01,
-                                                       unsigned logn, unsigned lvl, unsigned L,
-                                                       unsigned npoly, DownTable tab, Tw2 tw, const ModConst *mcs)
+                                                       const uint64_t *X, size_t x_pstride, unsigned logn,
+                                                       unsigned lvl, unsigned L, unsigned npoly, DownTable tab,
+                                                       Tw2 tw, const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
@@ -3652,21 +3253,10 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   const uint64_t *x = conv + (((size_t)p * keep) << logn) + toff;
   const uint64_t *xs = X + p * x_pstride + toff;
   const int th = threadIdx.x, row = th / T::TA, l = th % T::TA, h = th % T::TA;
-  uint64_t xv[8], dv[8];
-  int pos[8];
+  uint64_t xv[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    pos[i] = wl_elem(i);
-    xv[i] = xs[pos[i]];
-  }
-  if (d01.d01 || d01.a) {
-    d01_fetch8(d01, p, toff, pos, mc, dv);
-  } else {
-    // no d0/d1 source: the key switch added P (d0, d1) to X already (p_lo = 0)
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-      dv[i] = 0;
-  }
+  for (int i = 0; i < 8; i++)
+    xv[i] = xs[wl_elem(i)];
   uint64_t cv[8];
   with_arith(q, m, logn, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
@@ -3681,261 +3271,69 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   for (int k = 0; k < 8; k++)
     lds[T::at(row, 8 * h + k)] = cv[k];
   wave_sync();
-  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], f = tab.fin[2 * t], fp = tab.fin[2 * t + 1];
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t];
   uint64_t *o = out + p * out_pstride + toff;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const int e = wl_elem(i);
     const uint64_t c = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
     if (q < F64_QMAX) {
-      // exact FP64 products: |X - conv| < q, each product < 1.25 q
-      const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv), fd = f64_from_u52(f);
-      const double v = f64_mulmod(f64_from_u52(xv[i]) - f64_from_u52(c), di, di * qinv, qd) +
-                       f64_mulmod(f64_from_u52(dv[i]), fd, fd * qinv, qd);
-      o[e] = f64_canon(v, qd, qinv);
+      // exact FP64 product: |X - conv| < q, the product < 1.25 q
+      const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv);
+      o[e] = f64_canon(f64_mulmod(f64_from_u52(xv[i]) - f64_from_u52(c), di, di * qinv, qd), qd, qinv);
     } else {
-      const uint64_t v = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
-      o[e] = add_mod(v, mul_shoup(dv[i], f, fp, q), q);
+      o[e] = mul_shoup(sub_mod(xv[i], c, q), dinv, dinvp, q);
     }
   }
-}
-
-// Keep slots of the fused relinearization, deferred into the ModDown (the
-// accumulator's keep limbs never reach HBM).  A block owns (keep slot t, row
-// tile) and a run of ciphertexts with the key tile of both digits stationary
-// in LDS, as ks_rows2_kernel: per ciphertext the row pass of the non-own
-// digit's T1 limb and the MAC give X_0, X_1 (round C ownership, natural order)
-// in registers; then, per poly, the forward row pass of conv_t and the
-// dn_rows_kernel epilogue  out = (X - conv) Dprod^-1 + fin_t d01_t.
-// Inputs: T1 / d2 / key as ks_rows2_kernel, conv as dn_rows_kernel.
-template <int LOGN2>
-__global__ void __launch_bounds__(256, 2) kd_rows_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
-                                                          size_t d2_stride, const uint64_t *evkm,
-                                                          const uint64_t *conv, uint64_t *out, size_t out_pstride,
-                                                          D01Src d01, unsigned logn, unsigned lvl, unsigned L,
-                                                          unsigned nm, unsigned nmod, unsigned alpha, unsigned count,
-                                                          unsigned cpb, unsigned members, DownTable tab, Tw2 tw,
-                                                          const ModConst *mcs)
-{
-  using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
-  __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
-  const unsigned n1 = 1u << (logn - LOGN2);
-  const unsigned tiles = n1 / T::R;
-  const unsigned keep = tab.keep;
-  unsigned grp, mi;  // group = (keep slot t, tile) on one XCD; members = ciphertext runs
-  if (!xcd_group(members, keep * tiles, grp, mi))
-    return;
-  const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
-  if (p0 >= p1)
-    return;
-  const unsigned t = grp / tiles, tile = grp % tiles;
-  const unsigned m = basis_mod(t, lvl, L);
-  const ModConst mc = mcs[m];
-  const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * T::R;
-  const size_t toff = (size_t)row0 << LOGN2, loff = ((size_t)t << logn) + toff;
-  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
-  const unsigned own = t / alpha;  // t < lvl: digit `own` holds slot t as its NTT-form d2 limb
-  auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
-    if (j == own) {
-      // round C ownership is natural order: thread th holds words 8 th .. 8 th + 7
-      const ulonglong2 *v2 = (const ulonglong2 *)(d2n + p * d2_stride + loff + 8 * th);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const ulonglong2 w = v2[i];
-        x[2 * i] = w.x;
-        x[2 * i + 1] = w.y;
-      }
-    } else {
-      const uint64_t *s_ = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        x[k] = s_[(row << LOGN2) + l + T::TA * k];
-    }
-  };
-  const bool f64 = q < F64_QMAX && tw.fwdd;  // the key tile is plain for these moduli (to_mont_kernel)
-#pragma unroll
-  for (int c = 0; c < 4; c++)
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
-      kl[c][256 * k + th] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
-    }
-  uint64_t xn[2][8];
-  fetch(xn[0], 0, p0);
-  fetch(xn[1], 1, p0);
-  auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
-    const uint64_t lo = v * w, hi = mulhi64(v, w);
-    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
-    a = lazy_lt2q(a + r, q2);
-  };
-  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t], fin = tab.fin[2 * t], finp = tab.fin[2 * t + 1];
-  int pos[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    pos[k] = 8 * th + k;
-  with_arith(q, m, logn, tw, [&](const auto &ar) {
-    using A = std::decay_t<decltype(ar)>;
-    using V = typename A::V;
-    for (unsigned p = p0; p < p1; p++) {
-      uint64_t a0[8], a1[8];
-      V f0[8], f1[8];  // FP64 accumulators (|.| < 3q: two products of < 1.5q each)
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        V r[8];
-        wave_sync();  // the previous phase has finished with the LDS tile
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          r[k] = A::load(xn[j][k]);
-        if (p + 1 < p1)
-          fetch(xn[j], j, p + 1);  // prefetch: in flight during the rest of this ciphertext
-        if (j != (int)own)
-          rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
-        if constexpr (std::is_same<A, ArF64>::value) {
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
-            const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
-            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
-            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
-            f0[k] = j ? f0[k] + tb : tb;
-            f1[k] = j ? f1[k] + ta : ta;
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const uint64_t v = ar.canon(r[k]);
-            if (j == 0)
-              a0[k] = a1[k] = 0;
-            mac(a0[k], v, kl[2 * j][256 * k + th]);
-            mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
-          }
-        }
-      }
-      if constexpr (std::is_same<A, ArF64>::value) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          a0[k] = ar.canon(f0[k]);
-          a1[k] = ar.canon(f1[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
-          a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
-        }
-        (void)f0;
-        (void)f1;
-      }
-      // ModDown of both polys: conv_t row pass + epilogue (dn_rows_kernel)
-#pragma unroll
-      for (int half = 0; half < 2; half++) {
-        const unsigned P = 2 * p + half;
-        const uint64_t *x = conv + (((size_t)P * keep + t) << logn) + toff;
-        V r[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
-        uint64_t dv[8], cv[8];
-        d01_fetch8(d01, P, loff, pos, mc, dv);
-        wave_sync();
-        rows8_fwd<LOGN2>(r, cv, lds, ar, n1 + row0);
-        uint64_t o[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const uint64_t xv = half ? a1[k] : a0[k];
-          if (q < F64_QMAX) {
-            // exact FP64 products: |X - conv| < q, each product < 1.25 q
-            const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv), fd = f64_from_u52(fin);
-            const double v = f64_mulmod(f64_from_u52(xv) - f64_from_u52(cv[k]), di, di * qinv, qd) +
-                             f64_mulmod(f64_from_u52(dv[k]), fd, fd * qinv, qd);
-            o[k] = f64_canon(v, qd, qinv);
-          } else {
-            const uint64_t v = mul_shoup(sub_mod(xv, cv[k], q), dinv, dinvp, q);
-            o[k] = add_mod(v, mul_shoup(dv[k], fin, finp, q), q);
-          }
-        }
-        ulonglong2 *d2o = (ulonglong2 *)(out + P * out_pstride + loff + 8 * th);
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          d2o[i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
-      }
-    }
-  });
 }
 
 template <int LOGT1, int LOGN2>
 static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                            const D01Src &d01, unsigned npoly, unsigned lvl, DownTable &tab, const KsDeferred *ks)
+                            unsigned npoly, unsigned lvl, const DownTable &tab)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   {
-    // reads the nd row-transformed drop limbs, writes keep column-transformed limbs
+    // reads the nd row-transformed drop limbs, writes keep column-transformed
+    // limbs; NT = 8: one block per (poly, tile) owns every keep target, so
+    // the INTT columns run once
     ProfScope ps(KC_DN_COLS, 8.0 * n * npoly * (tab.nd + keep));
-    // NT = 8: one block per (poly, tile), the INTT columns run once; NT = 4
-    // (GPQHE_DN_NT=4): twice the blocks, the INTT columns run twice
-    static const unsigned nt = getenv("GPQHE_DN_NT") ? atoi(getenv("GPQHE_DN_NT")) : 8;
     constexpr unsigned NT = 8;
-    const unsigned members = (keep + nt - 1) / nt, ngroups = npoly * tiles;
+    const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, conv,
                          G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     };
-    auto go2 = [&](auto nt_c) {
-      constexpr unsigned N = decltype(nt_c)::value;
-      if (tab.f64 && (fbc64_mask() & 2))
-        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, N, false, true>) : go(dn_cols_kernel<LOGT1, N, true, true>);
-      else
-        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, N, false, false>) : go(dn_cols_kernel<LOGT1, N, true, false>);
-    };
-    if (nt == 4)
-      go2(std::integral_constant<unsigned, 4>{});
+    if (tab.f64 && FBC64_DN)
+      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true>) : go(dn_cols_kernel<LOGT1, NT, true, true>);
     else
-      go2(std::integral_constant<unsigned, NT>{});
+      tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false>) : go(dn_cols_kernel<LOGT1, NT, true, false>);
   }
-  if (ks) {
-    // keep slots' key-switch MAC here (ks_rows2 ran the drop slots only): reads
-    // per pair and keep slot the two digits' inputs, conv and the d0/d1 source
-    // of both polys, writes both; the key tiles once
-    const unsigned nm = lvl + G.K, count = npoly / 2, groups = keep * (n / 2048);
-    const unsigned members = std::max(1u, std::min(count, (6 * 256 + groups - 1) / groups));
-    const unsigned cpb = (count + members - 1) / members;
-    ProfScope ps(KC_KD_ROWS, 8.0 * n * ((double)count * keep * (2 + 2 + (d01.d01 ? 2.0 : 6.0) + 2) + 4.0 * keep));
-    hipLaunchKernelGGL((kd_rows_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, ks->T1,
-                       (size_t)2 * nm * n, ks->d2, (size_t)lvl * n, ks->evkm, conv, out, out_pstride, d01, G.logn, lvl,
-                       G.L, nm, G.nmod, G.alpha, count, cpb, members, tab, tw, G.dev.mc);
-    HIP_CHECK(hipGetLastError());
-    return;
-  }
-  // reads conv, X and the d0/d1 source (one limb, or lazily the products'
-  // factors: a0 b0 for d0, a0 a1 b0 b1 for d1), writes out
-  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * (d01.d01 ? 4.0 : d01.a ? 6.0 : 3.0));
+  // reads conv and X, writes out
+  ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 3.0);
   hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
-                     out, out_pstride, X, x_pstride, d01, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
+                     out, out_pstride, X, x_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode, const D01Src &d01, uint64_t *conv_ws, const KsDeferred *ks)
+                     int mode)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
-  DownTable &tab = down_table(lvl, mode);
+  const DownTable &tab = down_table(lvl, mode);
   if (tab.nd > 5)
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
-  uint64_t *conv = conv_ws ? conv_ws : (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
+  uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
-  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
-  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
-  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
-  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
-  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, d01, npoly, lvl, tab, ks); break;
+  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
+  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
+  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
+  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
+  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
-  if (!conv_ws)
-    pool_free(conv);
+  pool_free(conv);
 }
 
 // Benchmark input generator (oracle: poly_fill_uniform).
@@ -4021,8 +3419,6 @@ void tables_upload()
       id[2 * j + 1] = (double)itw[j] / qd;
     }
   }
-  if (getenv("GPQHE_NO_F64"))  // integer butterflies everywhere (A/B switch)
-    return;
   HIP_CHECK(hipMalloc((void **)&G.twd, 2 * nm * n * 8));
   HIP_CHECK(hipMalloc((void **)&G.itwd, 2 * nm * n * 8));
   HIP_CHECK(hipMemcpy((void *)G.twd, fd.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
@@ -4047,8 +3443,6 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.dig));
     HIP_CHECK(hipFree(kv.second.c));
     HIP_CHECK(hipFree(kv.second.ysc));
-    HIP_CHECK(hipFree(kv.second.ysc1));
-    HIP_CHECK(hipFree(kv.second.n2i));
     HIP_CHECK(hipFree(kv.second.cd));
   }
   g_up.clear();
@@ -4059,7 +3453,6 @@ void tables_free()
     HIP_CHECK(hipFree(kv.second.dinv));
     HIP_CHECK(hipFree(kv.second.dinvp));
     HIP_CHECK(hipFree(kv.second.ysc));
-    HIP_CHECK(hipFree(kv.second.fin));
     HIP_CHECK(hipFree(kv.second.cd));
   }
   g_down.clear();

@@ -27,6 +27,10 @@
 
 #include <stddef.h>
 #include <stdint.h>
+/* HECTR's sources call abort / exit / malloc without including <stdlib.h>
+   themselves (reference src/mpc.c:211, tests/hectr.c:938): the GPQHE header
+   they include provides it. */
+#include <stdlib.h>
 
 #ifdef __cplusplus
 extern "C" {

@@ -8,6 +8,7 @@
 #ifndef PMU_H
 #define PMU_H
 #include <stdio.h>
+#include <stdlib.h>
 #include <time.h>
 
 static inline double pmu_now_(void)

@@ -16,4 +16,4 @@ for f in sorted(glob.glob(f"gpurun_out/{sys.argv[1]}/bench_*.log")):
         t = d["ntt_roundtrip"]
         print(f"    ntt roundtrip {t['polys']} polys: {t['roundtrip_ms']:.2f} ms, {t['alg_GBs']:.0f} GB/s")
     for k, v in ks:
-        print(f"    {k:28s} {v['avg_us']:8.1f} us  {v['share']*100:5.1f}%  {v['GBs']:7.0f} GB/s")
+        print(f"    {k:28s} {v['avg_us']:8.1f} us  {v['share']*100:5.1f}%  {v['streamed_GBs']:7.0f} GB/s")

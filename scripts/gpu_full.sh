@@ -12,3 +12,9 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 cat $OUT/smoke.log
 RUN=${RUN:-full} bash scripts/gpu_prof.sh || exit 1
 tail -c 3000 $OUT/bench_full.log
+if [ -n "$FCAL" ]; then
+  # FETCH_SIZE / WRITE_SIZE calibration per access pattern (scripts/fetch_calib.py)
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fcal_fetch -o fcal_fetch --output-format csv -- ./scripts/ubench_mem > $OUT/fcal_fetch.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/fcal_write -o fcal_write --output-format csv -- ./scripts/ubench_mem > $OUT/fcal_write.log 2>&1 || exit 1
+  python scripts/fetch_calib.py $OUT > $OUT/fcal.txt 2>&1; cat $OUT/fcal.txt
+fi

@@ -14,5 +14,5 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 print("value", round(d["value"]), "alt", round(d.get("alt_primes", {}).get("value", 0)), "cstr", d.get("cstr", {}).get("steps_per_s"))
 for k, v in d["kernels"].items():
-    print(f"  {k:28s} {v['avg_us']:8.1f} us {v['GBs']:8.0f} GB/s")
+    print(f"  {k:28s} {v['avg_us']:8.1f} us {v['streamed_GBs']:8.0f} GB/s")
 PY

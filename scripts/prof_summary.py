@@ -2,14 +2,21 @@
 
     python scripts/prof_summary.py gpurun_out/<run> profiles/<tag>
 
-writes <tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats, as produced),
-<tag>_pmc.json (per kernel: launches, mean duration, HBM bytes per launch from
-FETCH_SIZE / WRITE_SIZE, L2 hit rate, SQ wait fractions) and, when the run
-has one, <tag>_bench.json (the default bench line of the same run).
+writes
+  <tag>_kernel_stats.csv      rocprofv3 --kernel-trace --stats of the short bench run, as produced
+  <tag>_ntt_kernel_stats.csv  the same for the config 2 NTT leg (scripts/prof_ntt.py)
+  <tag>_pmc.json              per kernel of the bench run: launches, mean duration, HBM bytes per
+                              launch, L2 hit rate, SQ wait / VALU fractions
+  <tag>_ntt_pmc.json          the same for the NTT leg
+  <tag>_bench.json            the default bench line of the same run (when present)
 
 Units and corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and
 WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
-coalesced streaming read, so fetch bytes = 2 x 1024 x FETCH_SIZE.
+coalesced streaming read, so fetch bytes = 2 x 1024 x FETCH_SIZE (validated
+per access width by scripts/ubench_mem.hip, profiles/r2_fetch_calibration.txt).
+VALU busy uses the gfx94x VALUBusy formula (ROCm 7.2 ships no gfx950 derived
+counters): SQ_ACTIVE_INST_VALU x 4 / SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs), with
+1024 SIMDs (256 CUs x 4); GRBM_GUI_ACTIVE is summed over the 8 XCDs.
 """
 import collections
 import csv
@@ -17,6 +24,9 @@ import json
 import os
 import shutil
 import sys
+
+SIMDS = 1024
+XCDS = 8
 
 
 def short(name):
@@ -33,15 +43,14 @@ def counters(path):
     return per
 
 
-def main(run, tag):
-    os.makedirs(os.path.dirname(tag) or ".", exist_ok=True)
-    shutil.copy(os.path.join(run, "kt", "kt_kernel_stats.csv"), tag + "_kernel_stats.csv")
+def summarise(run, prefix):
     dur = collections.defaultdict(list)
-    for r in csv.DictReader(open(os.path.join(run, "kt", "kt_kernel_trace.csv"))):
+    for r in csv.DictReader(open(os.path.join(run, prefix + "kt", prefix + "kt_kernel_trace.csv"))):
         dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     pmc = {}
     for f in ("fetch", "write", "hit", "sq"):
-        for k, cs in counters(os.path.join(run, f, f + "_counter_collection.csv")).items():
+        d = prefix + f
+        for k, cs in counters(os.path.join(run, d, d + "_counter_collection.csv")).items():
             for c, v in cs.items():
                 pmc.setdefault(k, {})[c] = sum(v) / len(v)
     out = {}
@@ -54,28 +63,51 @@ def main(run, tag):
             e["hbm_write_bytes"] = 1024 * c["WRITE_SIZE"]
         if "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             e["hbm_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+            e["hbm_GBs"] = e["hbm_bytes"] / e["mean_us"] / 1e3
         if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
             e["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
         if c.get("SQ_WAVE_CYCLES"):
-            for q in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
-                e[q.lower() + "_frac"] = c[q] / c["SQ_WAVE_CYCLES"]
+            for q in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+                if q in c:
+                    e[q.lower() + "_frac"] = c[q] / c["SQ_WAVE_CYCLES"]
+            e["sq_wait_any"] = e.get("sq_wait_any_frac")
+        if c.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in c:
+            e["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / (c["GRBM_GUI_ACTIVE"] / XCDS)
+            e["clock_GHz"] = c["GRBM_GUI_ACTIVE"] / XCDS / (e["mean_us"] * 1e3)
+        for q in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_BUSY_CYCLES"):
+            if q in c:
+                e[q.lower()] = c[q]
         out[k] = e
-    meta = {"source": run, "fetch_correction": "x2 (gfx950 FETCH_SIZE halves wide reads)", "units": "bytes per launch"}
-    bench_cfg = None
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["launches"]))
+
+
+def main(run, tag):
+    os.makedirs(os.path.dirname(tag) or ".", exist_ok=True)
+    meta = {"source": run, "fetch_correction": "x2 (gfx950 FETCH_SIZE halves wide reads)",
+            "units": "bytes per launch", "valu_busy": "SQ_ACTIVE_INST_VALU*4/1024/(GRBM_GUI_ACTIVE/8)"}
     full = os.path.join(run, "bench_full.log")
     if os.path.exists(full):
         lines = [l for l in open(full) if l.startswith('{"metric"')]
         if lines:
             b = json.loads(lines[-1])
             json.dump(b, open(tag + "_bench.json", "w"), indent=1)
-            bench_cfg = b["config"]["workload"]
-    meta["bench_workload"] = bench_cfg
-    json.dump({"meta": meta, "kernels": dict(sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["launches"]))},
-              open(tag + "_pmc.json", "w"), indent=1)
-    for k, e in sorted(out.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["launches"])[:14]:
-        print(f"{k:40s} n={e['launches']:4d} {e['mean_us']:8.1f} us  "
-              f"hbm={e.get('hbm_bytes', 0) / 1e6:8.1f} MB  l2hit={e.get('l2_hit_rate', 0):.2f} "
-              f"wait={e.get('sq_wait_any_frac', 0):.2f}")
+            meta["bench_workload"] = b["config"]["workload"]
+            meta["pairs_per_launch"] = b["config"].get("pairs_per_launch")
+    for prefix, suffix in (("", ""), ("ntt_", "_ntt")):
+        if not os.path.exists(os.path.join(run, prefix + "kt")):
+            continue
+        shutil.copy(os.path.join(run, prefix + "kt", prefix + "kt_kernel_stats.csv"), tag + suffix + "_kernel_stats.csv")
+        out = summarise(run, prefix)
+        m = dict(meta)
+        if prefix:
+            m = {k: v for k, v in meta.items() if k not in ("bench_workload", "pairs_per_launch")}
+            m["workload"] = "config 2: NTT -> INTT of 1024 polys, N=2^16, L=8 (scripts/prof_ntt.py)"
+        json.dump({"meta": m, "kernels": out}, open(tag + suffix + "_pmc.json", "w"), indent=1)
+        print(f"== {tag}{suffix}")
+        for k, e in list(out.items())[:14]:
+            print(f"{k:40s} n={e['launches']:4d} {e['mean_us']:8.1f} us  hbm={e.get('hbm_bytes', 0) / 1e6:8.1f} MB "
+                  f"({e.get('hbm_GBs', 0):6.0f} GB/s) l2hit={e.get('l2_hit_rate', 0):.2f} "
+                  f"wait={e.get('sq_wait_any_frac', 0) or 0:.2f} valu={e.get('valu_busy', 0):.2f}")
 
 
 if __name__ == "__main__":

@@ -80,6 +80,21 @@ __global__ void tile8(uint64_t *o, const uint64_t *x)
   for (int i = 0; i < 16; i++)
     o[base + threadIdx.x + 256 * i] = r[i] + 1;
 }
+// ks_rows2 / ntt3_rows input pattern at N2 = 256: 2048-element tile, thread
+// (row = t / 32, l = t % 32) reads words (row << 8) + l + 32 k, k < 8 (8 B lanes,
+// 256 contiguous bytes per half wave)
+__global__ void rows8w(uint64_t *o, const uint64_t *x)
+{
+  const size_t base = (size_t)blockIdx.x * 2048;
+  const int row = threadIdx.x / 32, l = threadIdx.x % 32;
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = x[base + (row << 8) + l + 32 * k];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    o[base + (row << 8) + l + 32 * k] = r[k] + 1;
+}
 __global__ void tile16(ulonglong2 *o, const ulonglong2 *x)
 {
   const size_t base = (size_t)blockIdx.x * 2048;
@@ -94,6 +109,9 @@ __global__ void tile16(ulonglong2 *o, const ulonglong2 *x)
   }
 }
 
+// Every kernel reads the 1 GiB buffer x once and writes the 1 GiB buffer o
+// once per launch, so a rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE pass over this
+// binary calibrates the counters per access pattern (scripts/fetch_calib.py).
 int main()
 {
   const size_t limbs = 2048, n = limbs << 16;  // 1 GiB per buffer
@@ -120,6 +138,7 @@ int main()
   run("copy16", [&] { hipLaunchKernelGGL(copy16, dim3(8192), dim3(256), 0, 0, (ulonglong2 *)o, (const ulonglong2 *)x, n / 2); });
   run("tile8", [&] { hipLaunchKernelGGL(tile8, dim3(n / 4096), dim3(256), 0, 0, o, x); });
   run("tile16", [&] { hipLaunchKernelGGL(tile16, dim3(n / 4096), dim3(256), 0, 0, (ulonglong2 *)o, (const ulonglong2 *)x); });
+  run("rows8w", [&] { hipLaunchKernelGGL(rows8w, dim3(n / 2048), dim3(256), 0, 0, o, x); });
   run("rows8", [&] { hipLaunchKernelGGL(rows8, dim3(n / 4096), dim3(256), 0, 0, o, x); });
   run("cols8", [&] { hipLaunchKernelGGL(cols8, dim3(limbs * 16), dim3(256), 0, 0, o, x); });
   run("cols16", [&] { hipLaunchKernelGGL(cols16, dim3(limbs * 8), dim3(512), 0, 0, (ulonglong2 *)o, (const ulonglong2 *)x); });

@@ -88,3 +88,34 @@ def test_two_rank_gloo_matches_single_process():
     assert tmax == 2.0
     single = _run_batch(0, GLOBAL)
     assert np.array_equal(gathered, single)
+
+
+def test_bench_self_launch_two_ranks():
+    """bench.py --gpus 2 without torchrun starts its own two rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), which meet over gloo, run the
+    barrier and the max-over-ranks reduction the timed region uses, and rank 0
+    prints one JSON line with n_gpus = 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2 and lines[0]["max_over_ranks"] == 2.0
+
+
+def test_bench_rejects_world_mismatch():
+    """Under an external launcher, --gpus must equal WORLD_SIZE (a scale run
+    must never silently time fewer ranks than it reports)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

@@ -1,0 +1,28 @@
+"""N1 on the MI355X: the unchanged HECTR harness binary (built in the CPU
+container from /root/reference by `make -C harness hectr`, see
+tests/test_hectr_caller.py) runs `test-hectr cstr-hempc` against the product
+libgpqhe.so (hectr_amd/lib).  Its decoded trajectory must match the
+reference's plaintext run within 1e-6 relative and equal the same binary's
+run on the CPU oracle bit for bit (same seed, bit-exact engine)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_hectr_caller import OUT, ROOT, compare_to_mpc, run_cstr_hempc
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(OUT, "test-hectr")
+
+
+@pytest.mark.skipif(not os.path.exists(BIN), reason="harness binary not built (make -C harness hectr needs the "
+                                                      "reference sources, present only in the build container)")
+def test_cstr_hempc_unchanged_on_mi355x(tmp_path, product):
+    rec, ms = run_cstr_hempc(os.path.join(ROOT, "hectr_amd", "lib"), tmp_path / "gpu")
+    dev = compare_to_mpc(rec)
+    assert dev < 1e-6, dev
+    ora, _ = run_cstr_hempc(os.path.join(OUT, "cpu"), tmp_path / "cpu")
+    assert np.array_equal(rec, ora), "GPU and oracle trajectories differ"
+    print(f"unchanged test-hectr cstr-hempc on MI355X: 40 steps in {ms} ms (harness pmu timer), "
+          f"max rel dev vs cstr-mpc.bin {dev:.2e}")

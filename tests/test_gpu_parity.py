@@ -17,6 +17,7 @@ Parameter sets:
           key-stationary two-digit inner product)
   c14/c15: n=2^14 (all primes < 2^51) and n=2^15 (60-bit q0/P: mixed FP64 and
           integer limbs), L=6, K=3, dnum=2 -- the other fused tilings
+  a5    : n=2^13, L=5, dnum=1 (one 5-limb digit), K=4
 Integer results must match exactly; decoded values are compared with the
 closed-loop tolerance of the CSTR test (1e-6 relative, reference achieves
 1e-11).
@@ -42,6 +43,9 @@ PARAMS = {
     # rows) and n=2^15 (128 x 256 columns, 256-element rows)
     "c14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
     "c15": ("params", dict(logn=15, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=60, qi_bits=48, p_bits=60)),
+    # one digit of 5 limbs (alpha > 4: the single-target ks_cols_kernel and the
+    # streaming ks_rows_kernel), n=2^13, L=5, dnum=1, K=4 (P 240 > 200 bits)
+    "a5": ("params", dict(logn=13, nlimbs=5, nspecial=4, dnum=1, slots=64, q0_bits=40, qi_bits=40, p_bits=60)),
 }
 
 
@@ -168,70 +172,70 @@ def test_ntt_batch_bitexact(oracle, product, name):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench_d2_rowform", "bench_d2_lanes", "bench51",
-                                  "bench51_tensor", "c5", "c17", "c14", "c15", "bench_d2_kd", "bench51_kd",
-                                  "bench51_tensor_kd", "c14_kd", "c15_kd", "c17_kd", "bench_d2_dnd",
-                                  "bench51_dnd", "bench51_tensor_dnd", "c15_dnd", "c5_dnd",
-                                  "bench_d2_noinvc", "bench51_noinvc", "c14_noinvc", "c15_noinvc"])
-def test_mul_rescale_batch_bitexact(oracle, product, name, monkeypatch):
-    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 and the bench's dnum=2/K=4, the
-    latter also through the opt-in row-form key switch and through the
-    two-stream chunk pipeline: 5 pairs in chunks of 2, and with d0/d1
-    materialized by the tensor kernel instead of formed by their consumers)
-    and the config 5 op at n=2^17, L=12 on random-residue ciphertext pairs.
-    "_kd": the opt-in path that moves the keep slots' key-switch MAC into the
-    ModDown rows (GPQHE_KDROWS, kd_rows_kernel)."""
+def mul_batch_both(oracle, product, name, cnt, lvl=None, seeds=(1, 2)):
+    """he_mul_rescale_batch of `cnt` random-residue pairs at level `lvl` on
+    both engines (same keys, same inputs); returns (oracle, product) outputs."""
     import ctypes
     import torch
-    cnt = 3
-    if name.endswith("_kd"):
-        monkeypatch.setenv("GPQHE_KDROWS", "1")
-        name = name[:-len("_kd")]
-    if name.endswith("_noinvc"):  # d2's INTT columns in ntt2_cols, not ks_cols4 (GPQHE_KSC_INVC=0)
-        monkeypatch.setenv("GPQHE_KSC_INVC", "0")
-        name = name[:-len("_noinvc")]
-    if name.endswith("_dnd"):  # d0/d1 added in the ModDown epilogue (GPQHE_D01_KS=0)
-        monkeypatch.setenv("GPQHE_D01_KS", "0")
-        name = name[:-len("_dnd")]
-    if name.endswith("_rowform"):
-        monkeypatch.setenv("GPQHE_KS_ROWFORM", "1")
-        name = name[:-len("_rowform")]
-    if name.endswith("_tensor"):
-        monkeypatch.setenv("GPQHE_TENSOR", "1")  # materialized d0/d1 (A/B path)
-        name = name[:-len("_tensor")]
-    if name.endswith("_lanes"):
-        monkeypatch.setenv("GPQHE_CHUNK", "2")
-        monkeypatch.setenv("GPQHE_LANES", "1")
-        name, cnt = name[:-len("_lanes")], 5
     init_both(oracle, product, name)
-    n, L = product.n, product.L
+    n = product.n
+    lvl = lvl or product.L
     _, _, _, rlk_o = keys(oracle, rot=False)
     _, _, _, rlk_p = keys(product, rot=False)
     same(oracle, product, rlk_o, rlk_p)
-    words = cnt * 2 * L * n
+    words = max(cnt, 1) * 2 * lvl * n
     a = np.zeros(words, dtype=np.uint64)
     b = np.zeros(words, dtype=np.uint64)
-    oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * cnt, L, 1)
-    oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * cnt, L, 2)
-    out_o = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
-    oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, L, ctypes.byref(rlk_o))
+    oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * max(cnt, 1), lvl, seeds[0])
+    oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * max(cnt, 1), lvl, seeds[1])
+    out_o = np.full(max(cnt, 1) * 2 * (lvl - 1) * n, 7, dtype=np.uint64)
+    oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, lvl, ctypes.byref(rlk_o))
     da = torch.from_numpy(a.view(np.int64)).cuda()
     db = torch.from_numpy(b.view(np.int64)).cuda()
-    dout = torch.zeros(out_o.size, dtype=torch.int64, device="cuda")
+    del a, b
+    dout = torch.full((out_o.size,), 7, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
-    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, L, ctypes.byref(rlk_p))
+    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, lvl, ctypes.byref(rlk_p))
     product.sync()
     got = dout.cpu().numpy().view(np.uint64)
-    assert np.array_equal(got, out_o), f"{np.count_nonzero(got != out_o)} residues differ"
+    del da, db, dout
+    return out_o, got
 
 
-def test_batch_real_encryptions_decode(product):
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c17", "c14", "c15", "a5"])
+def test_mul_rescale_batch_bitexact(oracle, product, name):
+    """Config 3 op at n=2^16, L=8 (dnum=8/K=1 through the streaming inner
+    product, the bench's dnum=2/K=4 with 60-bit and with < 2^51 primes), the
+    config 5 op at n=2^17, L=12, and the other fused tilings, on 3
+    random-residue pairs (one ks_rows2 run per pair)."""
+    want, got = mul_batch_both(oracle, product, name, 3)
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
+
+
+@pytest.mark.parametrize("name,cnt,chunk", [("bench51", 17, None), ("bench51", 24, None), ("bench_d2", 17, None),
+                                            ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None)])
+def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
+    """The headline shape (bench.py): n=2^16, L=8,
+    dnum=2, K=4 on 17 and 24 pairs (ks_rows2 runs of 5-6 ciphertexts: the
+    cross-ciphertext prefetch, key-tile reuse and accumulator restart), 17
+    pairs in chunks of 5/5/5/2 (the multi-chunk loop, a short last chunk) and
+    the bench's own 256 pairs (two 128-pair chunks of the 8 GiB workspace,
+    runs of 8), every output residue compared with the oracle."""
+    if chunk:
+        monkeypatch.setenv("GPQHE_CHUNK", str(chunk))
+    want, got = mul_batch_both(oracle, product, name, cnt, seeds=(21, 22))
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
+
+
+@pytest.mark.parametrize("name", ["bench_d2", "bench51"])
+def test_batch_real_encryptions_decode(product, name):
     """a 4-ciphertext subset of real encryptions of
     uniform reals in [-1, 1] through he_mul_rescale_batch decodes to the
-    slot-wise products (bench parameters, dnum=2/K=4)."""
+    slot-wise products, on the conventional 60-bit q0/P set and on the
+    bench's < 2^51 set (q0 51 bits at Delta = 2^50)."""
     import ctypes
     import torch
-    kind, kw = PARAMS["bench_d2"]
+    kind, kw = PARAMS[name]
     product.init_params(**kw)
     product.set_seed(9)
     pk, sk, _, rlk = keys(product, rot=False)
@@ -263,27 +267,8 @@ def test_mul_rescale_batch_levels(oracle, product, name, lvl, cnt):
     """The fused batch op below the top level (lvl 6: digits {0..3} {4,5},
     a partial digit; lvl 3: one partial digit), a batch of one pair and an
     empty batch (a no-op that must not touch the output)."""
-    import ctypes
-    import torch
-    init_both(oracle, product, name)
-    n = product.n
-    _, _, _, rlk_o = keys(oracle, rot=False)
-    _, _, _, rlk_p = keys(product, rot=False)
-    words = max(cnt, 1) * 2 * lvl * n
-    a = np.zeros(words, dtype=np.uint64)
-    b = np.zeros(words, dtype=np.uint64)
-    oracle.lib.poly_fill_uniform(a.ctypes.data, 2 * max(cnt, 1), lvl, 5)
-    oracle.lib.poly_fill_uniform(b.ctypes.data, 2 * max(cnt, 1), lvl, 6)
-    out_o = np.full(max(cnt, 1) * 2 * (lvl - 1) * n, 7, dtype=np.uint64)
-    oracle.lib.he_mul_rescale_batch(out_o.ctypes.data, a.ctypes.data, b.ctypes.data, cnt, lvl, ctypes.byref(rlk_o))
-    da = torch.from_numpy(a.view(np.int64)).cuda()
-    db = torch.from_numpy(b.view(np.int64)).cuda()
-    dout = torch.full((out_o.size,), 7, dtype=torch.int64, device="cuda")
-    torch.cuda.synchronize()
-    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), db.data_ptr(), cnt, lvl, ctypes.byref(rlk_p))
-    product.sync()
-    got = dout.cpu().numpy().view(np.uint64)
-    assert np.array_equal(got, out_o), f"{np.count_nonzero(got != out_o)} residues differ"
+    want, got = mul_batch_both(oracle, product, name, cnt, lvl=lvl, seeds=(5, 6))
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
     if cnt == 0:
         assert np.all(got == 7)
 
