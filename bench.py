@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # kernels of the fused he_mul_rescale_batch pipeline (n = 2^16: one launch each per chunk)
-PIPELINE = ("d2_rows_kernel", "ks_cols4_kernel", "ks_rows2_kernel", "dn_cols_kernel", "dn_rows_kernel")
+PIPELINE = ("d2_rows_kernel", "ks_cols4_kernel", "ksq_kernel<drop>", "dn_cols_kernel", "ksq_kernel<keep>")
 
 
 def parse(argv=None):
@@ -206,10 +206,24 @@ def pmc_profile(workload, pairs_per_launch):
     return None, None
 
 
+def kernel_key(name):
+    """Kernel identity shared by the library's own statistics and rocprofv3
+    names: the base name, plus <drop>/<keep> for the two ksq_kernel stages
+    (5th template argument KEEP)."""
+    base = name.split("<")[0].split("(")[0].strip()
+    if base == "ksq_kernel" and "<" in name:
+        args = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
+        if args in (["keep"], ["drop"]):
+            return f"ksq_kernel<{args[0]}>"
+        if len(args) >= 5:
+            return "ksq_kernel<keep>" if args[4] == "true" else "ksq_kernel<drop>"
+    return base
+
+
 def pmc_entry(prof, kernel):
-    base = kernel.split("<")[0]
+    key = kernel_key(kernel)
     for name, e in prof.get("kernels", {}).items():
-        if name.split("<")[0] == base and "hbm_bytes" in e:
+        if kernel_key(name) == key and "hbm_bytes" in e:
             return e
     return None
 

@@ -802,6 +802,29 @@ static void mul_chunk(uint64_t *out, size_t out_pstride, const uint64_t *a, cons
     gpqhe_die("relinearization key missing or built for another dnum");
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
+  if (k_mul_split_ok(lvl) && rlk->reserved) {
+    // split key switch: the kept slots' epilogue writes out while other pairs'
+    // inputs may still be unread, so out must not overlap the inputs -- except
+    // he_mul(c, c, b) on one pair, where every output word replaces the input
+    // word read by the same thread
+    const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
+    const unsigned keep = rescale ? lvl - 1 : lvl;
+    auto span = [](const uint64_t *p, size_t hi) { return std::make_pair((uintptr_t)p, (uintptr_t)(p + hi)); };
+    const auto o = span(out, (2 * (size_t)count - 1) * out_pstride + (size_t)keep * n);
+    const auto ia = span(a, (count - 1) * in_stride + in_pstride + (size_t)lvl * n);
+    const auto ib = span(b, (count - 1) * in_stride + in_pstride + (size_t)lvl * n);
+    auto overlap = [&](std::pair<uintptr_t, uintptr_t> x) { return o.first < x.second && x.first < o.second; };
+    const bool same_layout = count == 1 && out_pstride == in_pstride && (out == a || out == b);
+    if ((overlap(ia) || overlap(ib)) && !(same_layout && (!overlap(ia) || out == a) && (!overlap(ib) || out == b))) {
+      const size_t words = (2 * (size_t)count - 1) * out_pstride + (size_t)keep * n;
+      Ws tmp(words);
+      k_mul_relin_split(tmp.p, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale);
+      HIP_CHECK(hipMemcpyAsync(out, tmp.p, words * 8, hipMemcpyDeviceToDevice, G.stream));
+      return;
+    }
+    k_mul_relin_split(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale);
+    return;
+  }
   const size_t d2_stride = lvl * n, D_stride = (size_t)ndig * nm * n, acc_stride = 2 * nm * n;
   Ws d2(count * d2_stride), D(count * D_stride), acc(count * acc_stride);
   if (k_ks_fused_ok() && rlk->reserved) {

@@ -14,6 +14,7 @@
 // All other kernels are elementwise over (limb, coefficient) and stream HBM
 // with one 8-byte word per lane, canonical residues in and out.
 #include "gpqhe_internal.h"
+#include "ntt_device.h"
 
 #include <type_traits>
 
@@ -41,7 +42,7 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
   KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
-  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_KS_ROWS2, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_COUNT
+  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
@@ -49,8 +50,8 @@ static const char *kc_names[KC_COUNT] = {
   "ntt_whole_kernel<fwd>", "ntt_whole_kernel<inv>", "modup_kernel", "ks_inner_kernel", "tensor_kernel",
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "dn_cols_kernel", "dn_rows_kernel",
   "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
-  "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ks_rows2_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
-  "gemv_inner_kernel"};
+  "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
+  "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>"};
 
 struct ProfEntry {
   int cls;
@@ -323,348 +324,6 @@ __global__ void __launch_bounds__(TPB) ntt_whole_kernel(LimbSet s, unsigned logn
   }
 }
 
-// ===========================================================================
-// NTT v2 (two-pass, n = 2^13 .. 2^16): 4096-element tiles, 256 threads,
-// Harvey lazy butterflies (values in [0, 4q) inside a pass, canonical at every
-// pass boundary), interleaved (w, w') twiddle pairs (one 16-byte load), round
-// A loaded straight from HBM into registers, prime-major workgroup order so
-// the workgroups resident at one time share one prime's twiddle table.
-// ===========================================================================
-struct Tw2 {
-  const uint64_t *fwd;  // [nmod][n][2] (w, floor(w 2^64 / q))
-  const uint64_t *inv;
-  const double *fwdd;   // [nmod][n][2] (w, w / q) as doubles (moduli < 2^51)
-  const double *invd;
-};
-
-__device__ __forceinline__ uint64_t lazy_lt2q(uint64_t x, uint64_t q2)
-{
-  return x >= q2 ? x - q2 : x;
-}
-
-__device__ __forceinline__ uint64_t canon4(uint64_t x, uint64_t q, uint64_t q2)
-{
-  x = x >= q2 ? x - q2 : x;
-  return x >= q ? x - q : x;
-}
-
-// forward CT stages on E = 2^LE registers; twiddle run of stage s starts at
-// bb >> (log_thi - s + 1); inputs < 4q, outputs < 4q
-template <int LE>
-__device__ __forceinline__ void fwd_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
-                                           int log_thi, uint64_t q)
-{
-  constexpr int E = 1 << LE;
-  const uint64_t q2 = 2 * q;
-#pragma unroll
-  for (int s = 0; s < LE; s++) {
-    const uint64_t Bs = bb >> (log_thi - s + 1);
-    const int half = E >> (s + 1);
-#pragma unroll
-    for (int k = 0; k < E; k++) {
-      if (k & half)
-        continue;
-      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
-      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
-      const uint64_t U = lazy_lt2q(x[k], q2);
-      const uint64_t V = mul_shoup_lazy(x[k + half], w, wp, q);
-      x[k] = U + V;
-      x[k + half] = U - V + q2;
-    }
-  }
-}
-
-// inverse GS stages; inputs < 2q, outputs < 2q
-template <int LE>
-__device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
-                                           int log_tlo, uint64_t q)
-{
-  constexpr int E = 1 << LE;
-  const uint64_t q2 = 2 * q;
-#pragma unroll
-  for (int s = 0; s < LE; s++) {
-    const uint64_t Bs = bb >> (log_tlo + s + 1);
-    const int half = 1 << s;
-#pragma unroll
-    for (int k = 0; k < E; k++) {
-      if (k & half)
-        continue;
-      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
-      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
-      const uint64_t U = x[k], V = x[k + half];
-      x[k] = lazy_lt2q(U + V, q2);
-      x[k + half] = mul_shoup_lazy(U - V + q2, w, wp, q);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// FP64 butterflies for moduli q < 2^51 (the FP64 pipe is full rate on gfx950
-// and twice as fast as 64-bit integer Shoup per butterfly, scripts/ubench_bfly).
-// Values are signed doubles holding exact integers:
-//   mulmod: h = fl(y w), l = fma(y, w, -h) (exact), qt = rint(y fl(w/q)),
-//           T = fma(-qt, q, h) + l = y w - qt q exactly.  The quotient error
-//           is below 1/2 + |y| 2^-52, so for |y| <= 2q < 2^52 |T| < 1.5 q.
-//   red:    x - rint(x fl(1/q)) q, |result| <= q/2 (+ negligible).
-// CT: X = red(x[k]), T = mulmod(x[k+h]); outputs X +- T, |.| < 2q.
-// GS: outputs red(U + V) and mulmod(U - V) with |U - V| < 2q.
-// Every intermediate is an integer below 2^53, so the residues are exact and
-// the canonical outputs equal the integer path's bit for bit.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double f64_mulmod(double y, double w, double wq, double q)
-{
-  const double h = y * w;
-  const double l = __fma_rn(y, w, -h);
-  const double qt = rint(y * wq);
-  return __fma_rn(-qt, q, h) + l;
-}
-
-__device__ __forceinline__ double f64_red(double x, double q, double qinv)
-{
-  return __fma_rn(-rint(x * qinv), q, x);
-}
-
-// u64 <-> f64 for integers below 2^52 without the generic conversions (4 and
-// ~7 instructions): 2^52 + x has x as its mantissa bits.
-__device__ __forceinline__ double f64_from_u52(uint64_t x)
-{
-  return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 0x1p52;
-}
-
-// canonical residue of x (integer, |x| < 2^53): reduce, lift negatives by
-// q and read the mantissa of 2^52 + v
-__device__ __forceinline__ uint64_t f64_canon(double x, double q, double qinv)
-{
-  const double v = f64_red(x, q, qinv);
-  const double b = v < 0 ? q + 0x1p52 : 0x1p52;
-  return (uint64_t)__double_as_longlong(v + b) & ((1ull << 52) - 1);
-}
-
-template <int LE>
-__device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
-                                             int log_thi, double q, double qinv)
-{
-  constexpr int E = 1 << LE;
-#pragma unroll
-  for (int s = 0; s < LE; s++) {
-    const uint64_t Bs = bb >> (log_thi - s + 1);
-    const int half = E >> (s + 1);
-#pragma unroll
-    for (int k = 0; k < E; k++) {
-      if (k & half)
-        continue;
-      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
-      const double X = f64_red(x[k], q, qinv);
-      const double T = f64_mulmod(x[k + half], twd[i2], twd[i2 + 1], q);
-      x[k] = X + T;
-      x[k + half] = X - T;
-    }
-  }
-}
-
-template <int LE>
-__device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
-                                             int log_tlo, double q, double qinv)
-{
-  constexpr int E = 1 << LE;
-#pragma unroll
-  for (int s = 0; s < LE; s++) {
-    const uint64_t Bs = bb >> (log_tlo + s + 1);
-    const int half = 1 << s;
-#pragma unroll
-    for (int k = 0; k < E; k++) {
-      if (k & half)
-        continue;
-      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
-      const double U = x[k], V = x[k + half];
-      x[k] = f64_red(U + V, q, qinv);
-      x[k + half] = f64_mulmod(U - V, twd[i2], twd[i2 + 1], q);
-    }
-  }
-}
-
-// Arithmetic policies: the NTT kernels are written once against these.  Both
-// read and write canonical u64 residues; ArF64 requires q < 2^51.
-struct ArInt {
-  using V = uint64_t;
-  uint64_t q;
-  const uint64_t *tw;   // this modulus' forward (w, w') pairs
-  const uint64_t *itw;  // and inverse
-  __device__ static V load(uint64_t x) { return x; }
-  __device__ uint64_t canon(V x) const { return canon4(x, q, 2 * q); }  // x < 4q
-  __device__ static uint64_t bits(V x) { return x; }
-  __device__ static V unbits(uint64_t b) { return b; }
-  template <int LE>
-  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const { fwd_stages<LE>(x, tw, bb, log_thi, q); }
-  template <int LE>
-  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, itw, bb, log_tlo, q); }
-  // canonical x w for a constant w < q (Shoup pair)
-  __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
-  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t wp) const { return mulc(x, w, wp); }  // (FP64 only)
-};
-
-struct ArF64 {
-  using V = double;
-  double q, qinv;
-  const double *tw;   // this modulus' forward (w, w / q) pairs
-  const double *itw;  // and inverse
-  __device__ static V load(uint64_t x) { return f64_from_u52(x); }  // x canonical (< q)
-  __device__ uint64_t canon(V x) const { return f64_canon(x, q, qinv); }
-  __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
-  __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
-  template <int LE>
-  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
-  {
-    fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv);
-  }
-  template <int LE>
-  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
-  {
-    inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv);
-  }
-  __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
-  {
-    const double wd = f64_from_u52(w);
-    return canon(f64_mulmod(x, wd, wd / q, q));
-  }
-  // x w as the bits of a canonical double in [0, q) (FP64 basis conversion input)
-  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t) const
-  {
-    const double wd = f64_from_u52(w);
-    const double v = f64_red(f64_mulmod(x, wd, wd / q, q), q, qinv);
-    return (uint64_t)__double_as_longlong(v < 0 ? v + q : v);
-  }
-};
-
-// FP64 fast basis conversion term y c mod q_t for canonical y < q_i < 2^51 and
-// a constant c < q_t < 2^51 with cq = fl(c / q_t): y c / q_t < 2^51, so the
-// quotient estimate is off by at most 1, |result| <= q_t and every
-// intermediate is an integer below 2^53 (exact).  Sums of up to three terms
-// stay below 2^53; longer sums are reduced in between (f64_red).
-__device__ __forceinline__ double fbc_term(double y, double c, double cq, double q)
-{
-  return f64_mulmod(y, c, cq, q);
-}
-
-constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
-
-// Run f with the arithmetic policy of modulus index m (q = its prime).
-template <class F>
-__device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
-{
-  const size_t o = (size_t)m << (logn + 1);
-  if (q < F64_QMAX && tw.fwdd)
-    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
-  else
-    f(ArInt{q, tw.fwd + o, tw.inv + o});
-}
-
-// FP64 basis conversion (fbc_term) where it measured faster than the 128-bit
-// integer sums + REDC (same box, per 64-pair chunk at N=2^16, L=8): the INVC
-// ks_cols4 (323 vs 388 us) and dn_cols (296 vs 309 us).  The NT = 4 ks_cols4
-// (config 5) keeps the integer sums (308 vs 488 us with FP64).  Both forms are
-// exact, so the choice never changes a bit.
-constexpr bool FBC64_KS_INVC = true, FBC64_DN = true, FBC64_KS_NT4 = false;
-
-// with_arith for kernels instantiated per prime set: ALL_F64 (every modulus
-// < 2^51, FP64 tables present) keeps only the FP64 policy in the code.
-template <bool ALL_F64, class F>
-__device__ __forceinline__ void with_arith_t(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
-{
-  if constexpr (ALL_F64) {
-    const size_t o = (size_t)m << (logn + 1);
-    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
-  } else {
-    with_arith(q, m, logn, tw, f);
-  }
-}
-
-// Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
-// B reads 16 consecutive columns per thread at a 16-column lane stride; the
-// XOR spreads those lanes over distinct banks (8-way conflict without it).
-__device__ __forceinline__ int rswz(int c)
-{
-  return c ^ ((c >> 4) & 15);
-}
-
-// block -> (limb, tile) in prime-major order: all tiles of all limbs that use
-// basis slot t run before slot t + 1.
-__device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsigned &v, unsigned &tile)
-{
-  const unsigned groups = s.count / s.per;
-  const unsigned b = blockIdx.x;
-  const unsigned t = b / (groups * tiles);
-  const unsigned rem = b - t * groups * tiles;
-  const unsigned grp = rem / tiles;
-  tile = rem - grp * tiles;
-  v = grp * s.per + t;
-}
-
-// Column pass: tile = T rows x C columns (T C = 4096).
-template <int LOGT, bool INV, class A>
-__device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64_t *y, unsigned n2, uint64_t *lds,
-                                          uint64_t sw, uint64_t swp)
-{
-  using V = typename A::V;
-  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
-  const int t = threadIdx.x;
-  if constexpr (!INV) {
-    // round A: rows l + 16 k (distances T/2 .. 16)
-#pragma unroll
-    for (int it = 0; it < C / 16; it++) {
-      const int item = t + 256 * it, c = item % C, l = item / C;
-      const unsigned vo = (unsigned)l * n2 + c;  // 32-bit per-thread offset, uniform row bases
-      V r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = A::load((x + (size_t)(16 * k) * n2)[vo]);
-      ar.template fwd<LEA>(r, T, LOGT - 1);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        lds[(l + 16 * k) * CP + c] = A::bits(r[k]);
-    }
-    __syncthreads();
-    // round B: rows 16 g + k (distances 8 .. 1)
-    const int c = t % C, g = t / C;
-    const unsigned vo = (unsigned)(16 * g) * n2 + c;
-    V r[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      r[k] = A::unbits(lds[(16 * g + k) * CP + c]);
-    ar.template fwd<4>(r, T + 16 * g, 3);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      (y + (size_t)k * n2)[vo] = ar.canon(r[k]);
-  } else {
-    {
-      const int c = t % C, g = t / C;
-      const unsigned vo = (unsigned)(16 * g) * n2 + c;
-      V r[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        r[k] = A::load((x + (size_t)k * n2)[vo]);
-      ar.template inv<4>(r, T + 16 * g, 0);
-#pragma unroll
-      for (int k = 0; k < 16; k++)
-        lds[(16 * g + k) * CP + c] = A::bits(r[k]);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < C / 16; it++) {
-      const int item = t + 256 * it, c = item % C, l = item / C;
-      const unsigned vo = (unsigned)l * n2 + c;
-      V r[EA];
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        r[k] = A::unbits(lds[(l + 16 * k) * CP + c]);
-      ar.template inv<LEA>(r, T, 4);
-#pragma unroll
-      for (int k = 0; k < EA; k++)
-        (y + (size_t)(16 * k) * n2)[vo] = ar.mulc(r[k], sw, swp);
-    }
-  }
-}
-
 template <int LOGT, bool INV>
 __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                          const ModConst *mcs, const uint64_t *post)
@@ -688,269 +347,12 @@ __global__ void __launch_bounds__(256) ntt2_cols_kernel(LimbSet s, LimbSet o, un
   with_arith(mc.q, m, logn, tw, [&](const auto &ar) { cols_tile<LOGT, INV>(ar, x, y, n2, lds, sw, swp); });
 }
 
-// ---------------------------------------------------------------------------
-// Row pass, 8 elements per thread: tile = R x N2 with R N2 = 2048 (16 KiB of
-// LDS, no padding), three register rounds of 3, 3 and LOGN2 - 6 stages.
-// Half the registers of the 16-element form, so twice the waves per CU to
-// overlap one block's butterflies with another's loads.
-//   round A: thread (row, l < TA = N2/8)    elements l + TA k
-//   round B: thread (row, m < 8, l' < TA/8) elements m TA + l' + (TA/8) k
-//   round C: thread (row, h < TA)           elements 8 h + k (consecutive)
-// LDS swizzle (conflict-free for all four access patterns, checked offline):
-// column c of row r sits at c ^ ((c >> 3) & (TA - 1)) (^ (r & 1) << 4 for
-// N2 = 128).
-// ---------------------------------------------------------------------------
-// Every exchange of the 8-element row passes stays inside one row, and a
-// row belongs to one wave (TA = N2 / 8 threads per row, 64 / TA rows per
-// wave), so the row passes synchronise per wave, not per block: LDS
-// operations of one wave execute in order, the fences only keep the compiler
-// from moving them across the exchange.  Waves of a block never wait for each
-// other.
-__device__ __forceinline__ void wave_sync()
-{
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Word i < 8 of this thread in a wave-local coalesced walk over a
-// 2048-element row tile: wave w covers elements [512 w, 512 w + 512), which
-// are exactly its own rows.
-__device__ __forceinline__ int wl_elem(int i)
-{
-  return (threadIdx.x & ~63) * 8 + (threadIdx.x & 63) + 64 * i;
-}
-
-template <int LOGN2>
-struct Row8 {
-  static constexpr int N2 = 1 << LOGN2, R = 2048 / N2, TA = N2 / 8, TB = TA / 8, EC = 1 << (LOGN2 - 6);
-  static __device__ __forceinline__ int at(int row, int c)
-  {
-    int x = c ^ ((c >> 3) & (TA - 1));
-    if (LOGN2 == 7)
-      x ^= (row & 1) << 4;
-    return row * N2 + x;
-  }
-};
-
-// forward row pass of one tile, rounds A..C: round A input in r (the
-// thread's A elements), canonical result in out (the thread's C elements)
-// forward row pass of one tile leaving the thread's C elements lazy in r
-// (|.| < 2q for ArF64, < 4q for ArInt)
-template <int LOGN2, class A>
-__device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0)
-{
-  using T = Row8<LOGN2>;
-  using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA;
-  const uint64_t rb = (rowbase0 + row) << LOGN2;
-  {
-    const int l = th % T::TA;
-    ar.template fwd<3>(r, rb, LOGN2 - 1);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  {
-    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
-    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  const int h = th % T::TA;
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    r[k] = A::unbits(lds[T::at(row, 8 * h + k)]);
-#pragma unroll
-  for (int j = 0; j < 8 / T::EC; j++) {
-    V g[T::EC];
-#pragma unroll
-    for (int e = 0; e < T::EC; e++)
-      g[e] = r[j * T::EC + e];
-    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
-#pragma unroll
-    for (int e = 0; e < T::EC; e++)
-      r[j * T::EC + e] = g[e];
-  }
-}
-
-template <int LOGN2, class A>
-__device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)[8], uint64_t *lds, const A &ar,
-                                          uint64_t rowbase0)
-{
-  using T = Row8<LOGN2>;
-  using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA;
-  const uint64_t rb = (rowbase0 + row) << LOGN2;
-  {
-    const int l = th % T::TA;
-    ar.template fwd<3>(r, rb, LOGN2 - 1);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, l + T::TA * k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  {
-    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
-    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  const int h = th % T::TA;
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    r[k] = A::unbits(lds[T::at(row, 8 * h + k)]);
-#pragma unroll
-  for (int j = 0; j < 8 / T::EC; j++) {
-    V g[T::EC];
-#pragma unroll
-    for (int e = 0; e < T::EC; e++)
-      g[e] = r[j * T::EC + e];
-    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
-#pragma unroll
-    for (int e = 0; e < T::EC; e++)
-      out[j * T::EC + e] = ar.canon(g[e]);
-  }
-}
-
-// inverse row pass of one tile: input r = thread's C elements (canonical or
-// bounded as the policy's inverse allows), result r = thread's A elements
-// (lazy; canonicalise with ar.canon)
-template <int LOGN2, class A>
-__device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0)
-{
-  using T = Row8<LOGN2>;
-  using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA;
-  const uint64_t rb = (rowbase0 + row) << LOGN2;
-  {
-    const int h = th % T::TA;
-#pragma unroll
-    for (int j = 0; j < 8 / T::EC; j++) {
-      V g[T::EC];
-#pragma unroll
-      for (int e = 0; e < T::EC; e++)
-        g[e] = r[j * T::EC + e];
-      ar.template inv<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, 0);
-#pragma unroll
-      for (int e = 0; e < T::EC; e++)
-        r[j * T::EC + e] = g[e];
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, 8 * h + k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  {
-    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::unbits(lds[T::at(row, c0 + T::TB * k)]);
-    ar.template inv<3>(r, rb + mb * T::TA, LOGN2 - 6);
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, c0 + T::TB * k)] = A::bits(r[k]);
-  }
-  wave_sync();
-  {
-    const int l = th % T::TA;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::unbits(lds[T::at(row, l + T::TA * k)]);
-    ar.template inv<3>(r, rb, LOGN2 - 3);
-  }
-}
-
-// Inverse row pass of one tile whose words the thread already holds in the
-// wave-local coalesced order (raw[i] = word wl_elem(i)).
-template <int LOGN2, bool INV, class A>
-__device__ __forceinline__ void rows8_tile_raw(const A &ar, const uint64_t (&raw)[8], uint64_t *y, uint64_t *lds,
-                                               uint64_t rowbase0)
-{
-  static_assert(INV, "forward tiles load their own words");
-  using T = Row8<LOGN2>;
-  using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA, h = th % T::TA, l = th % T::TA;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int e = wl_elem(i);
-    lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = raw[i];
-  }
-  wave_sync();
-  V r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    r[k] = A::load(lds[T::at(row, 8 * h + k)]);
-  wave_sync();
-  rows8_inv<LOGN2>(r, lds, ar, rowbase0);
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
-}
-
-template <int LOGN2, bool INV, class A>
-__device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint64_t *y, uint64_t *lds,
-                                           uint64_t rowbase0)
-{
-  using T = Row8<LOGN2>;
-  using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA;
-  V r[8];
-  if constexpr (!INV) {
-    const int l = th % T::TA;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
-    uint64_t out[8];
-    rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0);
-    const int h = th % T::TA;
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      lds[T::at(row, 8 * h + k)] = out[k];
-    wave_sync();
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int e = wl_elem(i);
-      y[e] = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int e = wl_elem(i);
-      lds[T::at(e >> LOGN2, e & (T::N2 - 1))] = x[e];
-    }
-    wave_sync();
-    const int h = th % T::TA;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      r[k] = A::load(lds[T::at(row, 8 * h + k)]);
-    wave_sync();
-    rows8_inv<LOGN2>(r, lds, ar, rowbase0);
-    const int l = th % T::TA;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
-  }
-}
-
 template <int LOGN2, bool INV>
 __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                          const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T::WORDS];
   const unsigned n1 = 1u << (logn - LOGN2);
   unsigned v, tile;
   pm_decode(s, n1 / T::R, v, tile);
@@ -1870,10 +1272,6 @@ static UpTable &up_table(unsigned lvl)
   return g_up[lvl] = tab;
 }
 
-__device__ __forceinline__ unsigned basis_mod(unsigned t, unsigned lvl, unsigned L)
-{
-  return t < lvl ? t : L + (t - lvl);
-}
 
 // D[p][j][t][k] = FBC(digit j of xc[p]) mod basis_t (coefficient domain);
 // own limbs copy xc (the uniform NTT afterwards reproduces the NTT-domain
@@ -2074,23 +1472,6 @@ void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_strid
 // chunk).
 // ===========================================================================
 
-// XCD-aware grouping: workgroups are dealt round-robin over the 8 XCDs, so
-// blocks b and b + 8 share one XCD's L2.  Map block b to (group g, member i)
-// such that the `members` blocks of a group share b % 8 and are dispatched
-// close together; groups are padded to a multiple of 8 (extra blocks exit).
-// Placement only affects speed, never correctness.
-__device__ __forceinline__ bool xcd_group(unsigned members, unsigned ngroups, unsigned &g, unsigned &i)
-{
-  const unsigned b = blockIdx.x, x = b & 7, s = b >> 3;
-  i = s % members;
-  g = (s / members) * 8 + x;
-  return g < ngroups;
-}
-
-static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
-{
-  return ((ngroups + 7) / 8) * 8 * members;
-}
 
 template <int LOGT>
 __global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
@@ -2344,7 +1725,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
                                                        const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T::WORDS];
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
   unsigned grp, p;  // group = (basis slot t, tile) on one XCD; members = ciphertexts
@@ -2498,210 +1879,16 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
   });
 }
 
-// Key-stationary variant for two-digit keys (the bench's dnum = 2): a block
-// owns (basis slot t, row tile) and a run of ciphertexts [p0, p1).  The key
-// words of both digits stay in registers for the whole run (no per-ciphertext
-// key traffic), and the next ciphertext's two input tiles are prefetched into
-// registers while the current one is transformed and accumulated, so one load
-// latency is exposed per block instead of several per ciphertext.
-template <int LOGN2>
-__global__ void __launch_bounds__(256, 2) ks_rows2_kernel(const uint64_t *T1, size_t t1_stride, const uint64_t *d2n,
-                                                           size_t d2_stride, D01Src d01,
-                                                           const uint64_t *evkm, uint64_t *acc, size_t acc_stride,
-                                                           unsigned logn, unsigned lvl, unsigned L, unsigned nm,
-                                                           unsigned nmod, unsigned alpha, unsigned count,
-                                                           unsigned cpb, unsigned members, unsigned drop_lo,
-                                                           Tw2 tw, const ModConst *mcs)
-{
-  using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
-  __shared__ uint64_t kl[4][2048];  // key tile (b_0, a_0, b_1, a_1), thread-private order k 256 + th
-  const unsigned n1 = 1u << (logn - LOGN2);
-  const unsigned tiles = n1 / T::R;
-  unsigned grp, mi;  // group = (basis slot t, tile) on one XCD; members = ciphertext runs
-  if (!xcd_group(members, nm * tiles, grp, mi))
-    return;
-  const unsigned p0 = mi * cpb, p1 = min(count, p0 + cpb);
-  if (p0 >= p1)
-    return;
-  const unsigned t = grp / tiles, tile = grp % tiles;
-  const unsigned m = basis_mod(t, lvl, L);
-  const ModConst mc = mcs[m];
-  const uint64_t q = mc.q, q2 = 2 * q;
-  const unsigned row0 = tile * T::R;
-  const size_t toff = (size_t)row0 << LOGN2;
-  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
-  // digit j's input for ciphertext p: own digit -> the NTT-form d2 limb
-  // (natural layout, transposed through LDS), else T1[j][t] (row pass input)
-  const bool own0 = t < lvl && t / alpha == 0, own1 = t < lvl && t / alpha == 1;
-  const bool nat0 = own0, nat1 = own1;
-  auto src = [&](unsigned j, unsigned p) -> const uint64_t * {
-    const bool own = j ? own1 : own0;
-    return own ? d2n + p * d2_stride + ((size_t)t << logn) + toff
-               : T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
-  };
-  auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
-    const uint64_t *s_ = src(j, p);
-    if (j ? nat1 : nat0) {
-      // round C ownership is natural order: thread th holds words 8 th .. 8 th + 7
-      const ulonglong2 *v2 = (const ulonglong2 *)(s_ + 8 * th);
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const ulonglong2 w = v2[i];
-        x[2 * i] = w.x;
-        x[2 * i + 1] = w.y;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        x[k] = s_[(row << LOGN2) + l + T::TA * k];
-    }
-  };
-  const bool f64 = q < F64_QMAX && tw.fwdd;  // the key tile is plain for these moduli (to_mont_kernel)
-#pragma unroll
-  for (int c = 0; c < 4; c++)
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + th + 256 * k];
-      kl[c][256 * k + th] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
-    }
-  uint64_t xn[2][8];
-  fetch(xn[0], 0, p0);
-  fetch(xn[1], 1, p0);
-  auto mac = [&](uint64_t &a, uint64_t v, uint64_t w) {
-    const uint64_t lo = v * w, hi = mulhi64(v, w);
-    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
-    a = lazy_lt2q(a + r, q2);
-  };
-  with_arith(q, m, logn, tw, [&](const auto &ar) {
-    using A = std::decay_t<decltype(ar)>;
-    using V = typename A::V;
-    for (unsigned p = p0; p < p1; p++) {
-      uint64_t a0[8], a1[8];
-      V f0[8], f1[8];  // FP64 accumulators (|.| < 3q: two products of < 1.5q each)
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        V r[8];
-        wave_sync();  // the previous phase has finished with the LDS tile
-        if (j ? nat1 : nat0) {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            r[k] = A::load(xn[j][k]);
-          if (p + 1 < p1)
-            fetch(xn[j], j, p + 1);  // prefetch: in flight during the rest of this ciphertext
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            r[k] = A::load(xn[j][k]);
-          if (p + 1 < p1)
-            fetch(xn[j], j, p + 1);
-          rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
-        }
-        if constexpr (std::is_same<A, ArF64>::value) {
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
-            const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
-            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
-            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
-            f0[k] = j ? f0[k] + tb : tb;
-            f1[k] = j ? f1[k] + ta : ta;
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const uint64_t v = ar.canon(r[k]);
-            if (j == 0) {
-              a0[k] = a1[k] = 0;
-            }
-            mac(a0[k], v, kl[2 * j][256 * k + th]);
-            mac(a1[k], v, kl[2 * j + 1][256 * k + th]);
-          }
-        }
-      }
-      bool folded = false;  // P (d0, d1) added in FP64 before canonicalising
-      if constexpr (std::is_same<A, ArF64>::value) {
-        if (t < lvl) {
-          d01_fold_f64(d01, p, ((size_t)t << logn) + toff + 8 * th, mc, f0, f1);
-          folded = true;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          a0[k] = ar.canon(f0[k]);
-          a1[k] = ar.canon(f1[k]);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
-          a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
-        }
-        (void)f0;
-        (void)f1;
-      }
-      if (!folded && t < lvl) {
-        // round C ownership is natural order: words 8 th .. 8 th + 7
-        int pos[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          pos[k] = 8 * th + k;
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-          uint64_t c[8];
-          d01_fetch8(d01, 2 * p + half, ((size_t)t << logn) + toff, pos, mc, c);
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const uint64_t cv = mul_shoup(c[k], mc.pmod, mc.pmodp, q);
-            if (half)
-              a1[k] = add_mod(a1[k], cv, q);
-            else
-              a0[k] = add_mod(a0[k], cv, q);
-          }
-        }
-      }
-      uint64_t *o0 = acc + p * acc_stride + ((size_t)t << logn) + toff;
-      uint64_t *o1 = o0 + ((size_t)nm << logn);
-      if (t < drop_lo) {
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-          ulonglong2 *d2 = (ulonglong2 *)((half ? o1 : o0) + 8 * th);
-#pragma unroll
-          for (int i = 0; i < 4; i++)
-            d2[i] = half ? make_ulonglong2(a1[2 * i], a1[2 * i + 1]) : make_ulonglong2(a0[2 * i], a0[2 * i + 1]);
-        }
-      } else {
-        // limb dropped by the following ModDown: inverse row pass (dn_cols
-        // finishes the INTT)
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-          V r[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            r[k] = A::load(half ? a1[k] : a0[k]);
-          wave_sync();
-          rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
-          uint64_t *dst = half ? o1 : o0;
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            dst[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
-        }
-      }
-    }
-  });
-}
-
-
-template <int LOGT1, int LOGN2>
-static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
-                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned drop_lo,
-                            bool invc)
+// ModUp of d2 (its INTT finished here when invc) into T1 [count][ndig][nm]:
+// the digit's limbs converted to every other basis slot, forward column pass.
+template <int LOGT1>
+static void ks_cols_stage(const uint64_t *y, uint64_t *T1, unsigned count, unsigned lvl, bool invc)
 {
   // invc: y holds only the inverse row pass of d2 (d2_rows_kernel, unscaled);
   // ks_cols4 runs the inverse column pass with the full n^-1 [(Qj/q_i)^-1]
   const UpTable &tab = up_table(lvl);
   const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
-  const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n,
-               acc_stride = 2 * (size_t)nm * n;
+  const size_t y_stride = (size_t)lvl * n, t1_stride = (size_t)ndig * nm * n;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned tiles = n / 4096;
   const double own = (double)G.alpha * ndig;  // digit slots not converted (approx. for partial digits)
@@ -2734,33 +1921,31 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
                          y_stride, T1, t1_stride, G.logn, lvl, G.L, nm, ndig, ngroups, tab, tw, G.dev.mc);
     }
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int LOGT1, int LOGN2>
+static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n, const D01Src &d01,
+                            const uint64_t *evkm, uint64_t *acc, unsigned count, unsigned lvl, unsigned drop_lo,
+                            bool invc)
+{
+  ks_cols_stage<LOGT1>(y, T1, count, lvl, invc);
+  const UpTable &tab = up_table(lvl);
+  const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
+  const size_t t1_stride = (size_t)ndig * nm * n, d2_stride = (size_t)lvl * n, acc_stride = 2 * (size_t)nm * n;
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   // reads T1 (+ own d2 limbs, the four input limbs of d0/d1 on q limbs) per
   // ciphertext and the key once, writes acc
-  const bool rows2 = ndig == 2;
-  ProfScope ps(rows2 ? KC_KS_ROWS2 : KC_KS_ROWS,
-               8.0 * n * ((double)count * (ndig * nm + 4.0 * lvl + 2 * nm) + 2.0 * ndig * nm));
-  if (rows2) {
-    // key-stationary: runs of about 8 ciphertexts per block (64 pairs: 693 vs
-    // 712 us for runs of 13), more and shorter runs when the batch is too small
-    // to fill the GPU (~6 blocks per CU over (slot, tile) groups x runs)
-    const unsigned groups = nm * (n / 2048);
-    const unsigned fill = std::min(count, (6 * 256 + groups - 1) / groups);
-    const unsigned members = std::max(1u, std::max((count + 7) / 8, fill));
-    const unsigned cpb = (count + members - 1) / members;
-    hipLaunchKernelGGL((ks_rows2_kernel<LOGN2>), dim3(xcd_blocks(members, groups)), dim3(256), 0, G.stream, T1,
-                       t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod, G.alpha,
-                       count, cpb, members, drop_lo, tw, G.dev.mc);
-  } else {
-    hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream,
-                       T1, t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod, ndig,
-                       G.alpha, count, drop_lo, tw, G.dev.mc);
-  }
+  ProfScope ps(KC_KS_ROWS, 8.0 * n * ((double)count * (ndig * nm + 4.0 * lvl + 2 * nm) + 2.0 * ndig * nm));
+  hipLaunchKernelGGL((ks_rows_kernel<LOGN2>), dim3(xcd_blocks(count, nm * (n / 2048))), dim3(256), 0, G.stream, T1,
+                     t1_stride, d2n, d2_stride, d01, evkm, acc, acc_stride, G.logn, lvl, G.L, nm, G.nmod, ndig,
+                     G.alpha, count, drop_lo, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
 // d2 = a1 b1 of `count` pairs fused with the INTT's inverse row pass: block
 // = (limb, pair, 2048-element row tile), limb-major (one modulus' twiddles
-// hot at a time).  Writes the NTT-form d2 (the own-digit limbs of ks_rows2)
+// hot at a time).  Writes the NTT-form d2 when asked (the own-digit limbs of ks_rows)
 // and its inverse row pass (the column pass completes the INTT); replaces the
 // tensor kernel and the separate row pass (d0, d1 are formed by their
 // consumers, D01Src).
@@ -2771,7 +1956,7 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
                                                        const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T::WORDS];
   const unsigned n1 = 1u << (logn - LOGN2), tiles = n1 / T::R;
   const unsigned blk = blockIdx.x, limb = blk / (count * tiles), rem = blk - limb * count * tiles;
   const unsigned p = rem / tiles, tile = rem - p * tiles;
@@ -2779,13 +1964,15 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   const unsigned row0 = tile * T::R;
   const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
   const uint64_t *pa = a + p * in_stride + in_pstride + off, *pb = b + p * in_stride + in_pstride + off;
-  uint64_t *dn = d2 + (size_t)p * lvl * ((size_t)1 << logn) + off;
   uint64_t raw[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const int e = wl_elem(i);
-    raw[i] = mulmod_vv(pa[e], pb[e], mc);
-    dn[e] = raw[i];
+  for (int i = 0; i < 8; i++)
+    raw[i] = mulmod_vv(pa[wl_elem(i)], pb[wl_elem(i)], mc);
+  if (d2) {  // the NTT-form copy for the streaming ks_rows (the split key switch forms it from a, b)
+    uint64_t *dn = d2 + (size_t)p * lvl * ((size_t)1 << logn) + off;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      dn[wl_elem(i)] = raw[i];
   }
   uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
   with_arith(mc.q, limb, logn, tw, [&](const auto &ar) { rows8_tile_raw<LOGN2, true>(ar, raw, yo, lds, n1 + row0); });
@@ -2805,8 +1992,8 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned n = G.n;
   {
-    // reads a1, b1; writes d2 and its inverse row pass
-    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * 4);
+    // reads a1, b1; writes its inverse row pass (and d2 when asked)
+    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * (d2 ? 4 : 3));
     hipLaunchKernelGGL((d2_rows_kernel<LOGN2>), dim3(lvl * count * (n / 2048)), dim3(256), 0, G.stream, d2, ybuf, a,
                        b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc);
   }
@@ -3070,7 +2257,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 // combine is the row pass's epilogue.
 // ===========================================================================
 template <int LOGT, int NT, bool X5, bool F64>
-__global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, uint64_t *conv,
+__global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, size_t x_off, uint64_t *conv,
                                                           unsigned logn, unsigned lvl, unsigned L, unsigned members,
                                                           unsigned ngroups, DownTable tab, Tw2 tw,
                                                           const ModConst *mcs)
@@ -3088,7 +2275,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
   const unsigned keep = tab.keep, nd = tab.nd;
   if (mi * NT >= keep)
     return;
-  const uint64_t *yb = X + p * x_pstride + ((size_t)keep << logn) + (size_t)tile * C;
+  const uint64_t *yb = X + p * x_pstride + x_off + (size_t)tile * C;
   const int th = threadIdx.x;
   // Drop limbs arrive after the inverse row pass (ks_rows); the inverse column
   // pass with n^-1 [(Dprod/d)^-1]_d runs here.  Limbs 0..3 stay in registers.
@@ -3237,7 +2424,7 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
                                                        Tw2 tw, const ModConst *mcs)
 {
   using T = Row8<LOGN2>;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2048];
+  __shared__ __attribute__((aligned(16))) uint64_t lds[T::WORDS];
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
   const unsigned keep = tab.keep;
@@ -3269,14 +2456,14 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   wave_sync();
 #pragma unroll
   for (int k = 0; k < 8; k++)
-    lds[T::at(row, 8 * h + k)] = cv[k];
+    lds[T::at2(row, 8 * h, k)] = cv[k];
   wave_sync();
   const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t];
   uint64_t *o = out + p * out_pstride + toff;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const int e = wl_elem(i);
-    const uint64_t c = lds[T::at(e >> LOGN2, e & (T::N2 - 1))];
+    const uint64_t c = lds[T::wl(th, i)];
     if (q < F64_QMAX) {
       // exact FP64 product: |X - conv| < q, the product < 1.25 q
       const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv);
@@ -3287,9 +2474,11 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   }
 }
 
-template <int LOGT1, int LOGN2>
-static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                            unsigned npoly, unsigned lvl, const DownTable &tab)
+// conv [npoly][keep] <- forward column pass of FBC(INTT(drop limbs)); the drop
+// limbs of poly p sit at X + p x_pstride + x_off (inverse row pass done)
+template <int LOGT1>
+static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, size_t x_off, unsigned npoly,
+                          unsigned lvl, const DownTable &tab)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
@@ -3301,14 +2490,24 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
     constexpr unsigned NT = 8;
     const unsigned members = (keep + NT - 1) / NT, ngroups = npoly * tiles;
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, conv,
-                         G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
+      hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, x_off,
+                         conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     };
     if (tab.f64 && FBC64_DN)
       tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true>) : go(dn_cols_kernel<LOGT1, NT, true, true>);
     else
       tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false>) : go(dn_cols_kernel<LOGT1, NT, true, false>);
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int LOGT1, int LOGN2>
+static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
+                            unsigned npoly, unsigned lvl, const DownTable &tab)
+{
+  const unsigned n = G.n, keep = tab.keep;
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  dn_cols_stage<LOGT1>(conv, X, x_pstride, (size_t)keep << G.logn, npoly, lvl, tab);
   // reads conv and X, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 3.0);
   hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
@@ -3334,6 +2533,85 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
   pool_free(conv);
+}
+
+// ===========================================================================
+// ct x ct relinearization [+ rescale] of `count` pairs, split key switch:
+//   d2_rows  d2 = a1 b1, inverse row pass                  -> y
+//   ks_cols4 inverse column pass, ModUp conversion, forward column pass -> T1
+//   ksq<drop> key inner product of the dropped slots, inverse row pass -> accd
+//   dn_cols  their INTT + conversion to the kept slots, forward column pass -> conv
+//   ksq<keep> key inner product of the kept slots + P (d0, d1), minus
+//             NTTrows(conv), times D^-1                       -> out
+// The kept slots' accumulators never reach HBM.  Digits per key: 1 or 2.
+// ===========================================================================
+static bool split_ndig_ok(unsigned ndig)
+{
+  // the key tile (2 ndig x 16 KB), three padded row tiles (3 x 18 KB) and the
+  // row twiddles (32 KB) fit the LDS for one and two digits; longer keys take
+  // the streaming ks_rows path (config 5, dnum = 3: 7.4k vs 6.8k ct-mult/s
+  // without staged twiddles, same box)
+  return ndig >= 1 && ndig <= 2;
+}
+
+bool k_mul_split_ok(unsigned lvl)
+{
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha;
+  return k_ks_fused_ok() && split_ndig_ok(ndig);
+}
+
+template <int LOGT1, int LOGN2>
+static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
+                             size_t in_stride, size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl,
+                             bool rescale)
+{
+  const UpTable &up = up_table(lvl);
+  const DownTable &dn = down_table(lvl, rescale ? 1 : 0);
+  const unsigned nm = up.nm, ndig = up.ndig, keep = dn.keep, nd = dn.nd, n = G.n;
+  if (nd > 5)
+    gpqhe_die("split key switch: ModDown over %u moduli unsupported (max 5)", nd);
+  const unsigned na_min = lvl - (ndig - 1) * G.alpha;
+  const bool invc = G.alpha <= 4 && nm - na_min <= 8;
+  uint64_t *y = (uint64_t *)pool_alloc((size_t)count * lvl * n * 8);
+  uint64_t *T1 = (uint64_t *)pool_alloc((size_t)count * ndig * nm * n * 8);
+  uint64_t *accd = (uint64_t *)pool_alloc((size_t)2 * count * nd * n * 8);
+  uint64_t *conv = (uint64_t *)pool_alloc((size_t)2 * count * keep * n * 8);
+  const D01Src d01{a, b, in_stride, in_pstride};
+  const bool allf = up.f64 && dn.f64;
+  d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc);
+  ks_cols_stage<LOGT1>(y, T1, count, lvl, invc);
+  {
+    // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per
+    // workgroup; writes the inverse row pass of the nd dropped slots
+    ProfScope ps(KC_KSQ_DROP, 8.0 * n * count * ((double)ndig * nd + 2.0 * nd + (rescale ? 4.0 - 1.0 : 0.0)));
+    ksq_run(LOGN2, ndig, allf, false, T1, d01, evkm, accd, (size_t)nd * n, nullptr, dn.dinv, dn.dinvp, count, lvl,
+            nm, keep, nd);
+  }
+  dn_cols_stage<LOGT1>(conv, accd, (size_t)nd * n, 0, 2 * count, lvl, dn);
+  {
+    // reads T1 (ndig - 1 converted limbs), the four input limbs and the two
+    // conv limbs per pair and kept slot; writes the two output limbs
+    ProfScope ps(KC_KSQ_KEEP, 8.0 * n * count * keep * ((double)ndig - 1.0 + 4.0 + 2.0 + 2.0));
+    ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.dinv, dn.dinvp, count, lvl, nm, 0,
+            keep);
+  }
+  pool_free(conv);
+  pool_free(accd);
+  pool_free(T1);
+  pool_free(y);
+}
+
+void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
+                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale)
+{
+  switch (G.logn) {
+  case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 16: mul_split_launch<8, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  default: gpqhe_die("split key switch needs 2^13 <= n <= 2^17");
+  }
 }
 
 // Benchmark input generator (oracle: poly_fill_uniform).

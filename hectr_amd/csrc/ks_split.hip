@@ -1,0 +1,355 @@
+// ks_split.hip - the split key switch's inner-product kernels (gfx950): the
+// dropped basis slots (inverse row pass out) and the kept slots (ModDown
+// epilogue fused).  Orchestrated by kernels.hip:mul_split_launch.
+#include "ntt_device.h"
+
+#include <algorithm>
+
+// ===========================================================================
+// Key switch split at the ModDown boundary, key tile shared by quarter streams.
+//
+// One workgroup of QN x 256 threads owns a (basis slot t, 2048-element row
+// tile) and a range of ciphertext pairs; each 256-thread quarter works through
+// its own pairs (p = first + quarter + QN k) on its own LDS row tile, and the
+// key words of every digit for (t, tile) are loaded into LDS once per
+// workgroup and read by all quarters.  That keeps the key stationary (no
+// per-pair key traffic) at QN waves per SIMD instead of the two that one
+// 80 KB private key tile per 256 threads allows.
+//
+// Per pair and slot t: f0, f1 = sum over digits j of x_j (b_j, a_j)[t], x_j
+// the forward row pass of the converted limb T1[j][t], or for the digit that
+// owns a q limb t, d2 = a1 b1 itself (NTT domain, formed from the inputs: no
+// d2 copy); on q limbs + P (d0, d1) with d0 = a0 b0, d1 = a0 b1 + a1 b0.
+//   KEEP = false (slots t >= drop_lo, the limbs the ModDown divides out): the
+//     inverse row pass of (f0, f1) goes to accd (dn_cols finishes the INTT
+//     and converts).
+//   KEEP = true (t < drop_lo): the ModDown epilogue follows at once, so the
+//     accumulators never reach HBM: out = (f - NTTrows(conv)) D^-1 with conv
+//     from dn_cols (the key switch of the dropped limbs ran first).
+// Inputs a, b are read here and by d2_rows only; out may alias them when each
+// output word sits where the same pair's input word of the same slot was
+// (he_mul(c, c, b)): the thread that writes it has read it.
+// ===========================================================================
+template <int LOGN2, int NDIG, int QN, bool ALLF, bool KEEP, bool LTW>
+__global__ void __launch_bounds__(256 * QN, 1)
+    ksq_kernel(const uint64_t *T1, size_t t1_stride, D01Src d01, const uint64_t *evkm, uint64_t *dst,
+               size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp, unsigned logn,
+               unsigned lvl, unsigned L, unsigned nm, unsigned nmod, unsigned alpha, unsigned count, unsigned members,
+               unsigned t_lo, unsigned t_n, Tw2 tw, const ModConst *mcs)
+{
+  using T = Row8<LOGN2>;
+  constexpr int NX = KEEP ? NDIG - 1 : NDIG;  // converted limbs per slot at most
+  __shared__ __attribute__((aligned(16))) uint64_t kl[2 * NDIG][2048];  // (b_j, a_j), order k 256 + th
+  __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];    // row tile per quarter
+  // LTW: the tile's row-pass twiddles (RowTw), read by every quarter: with
+  // every modulus on FP64 (ALLF) forward and inverse as 8-byte entries, else
+  // the forward ones as 16-byte entries
+  constexpr int TWW = !LTW ? 2 : ALLF ? 2 * RowTw<LOGN2>::ENTRIES : 2 * RowTw<LOGN2>::ENTRIES;
+  __shared__ __attribute__((aligned(16))) uint64_t rtw[TWW];
+  const unsigned n1 = 1u << (logn - LOGN2);
+  const unsigned tiles = n1 / T::R;
+  unsigned grp, mi;  // group = (slot, tile) on one XCD; members = pair ranges
+  if (!xcd_group(members, t_n * tiles, grp, mi))
+    return;
+  const unsigned pb0 = (unsigned)(((size_t)mi * count) / members), pb1 = (unsigned)(((size_t)(mi + 1) * count) / members);
+  if (pb0 >= pb1)
+    return;
+  const unsigned t = t_lo + grp / tiles, tile = grp % tiles;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t q = mc.q, q2 = 2 * q;
+  const unsigned row0 = tile * T::R;
+  const size_t toff = (size_t)row0 << LOGN2;
+  const bool f64 = ALLF || (q < F64_QMAX && tw.fwdd);  // key words as plain doubles (to_mont_kernel)
+  for (unsigned idx = threadIdx.x; idx < 2 * NDIG * 2048; idx += 256 * QN) {
+    const unsigned c = idx >> 11, w = idx & 2047;
+    const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + w];
+    kl[c][w] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
+  }
+  __syncthreads();
+  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  uint64_t *lq = rt[qi];
+  const unsigned jo = t < lvl ? t / alpha : NDIG;  // the digit owning q limb t (none on P limbs)
+  const int nx = jo < NDIG ? NDIG - 1 : NDIG;
+  auto jof = [&](int u) -> unsigned { return (unsigned)u < jo ? (unsigned)u : (unsigned)u + 1; };
+  auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
+    const uint64_t *s = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      x[k] = s[(row << LOGN2) + l + T::TA * k];
+  };
+  unsigned p = pb0 + qi;
+  uint64_t xn[NX > 0 ? NX : 1][8];
+  if (p < pb1)
+#pragma unroll
+    for (int u = 0; u < NX; u++)
+      if (u < nx)
+        fetch(xn[u], jof(u), p);
+  auto mac_i = [&](uint64_t &a, uint64_t v, uint64_t w) {  // Montgomery MAC, lazy [0, 2q)
+    const uint64_t lo = v * w, hi = mulhi64(v, w);
+    const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
+    a = lazy_lt2q(a + r, q2);
+  };
+  with_arith_t<ALLF>(q, m, logn, tw, [&](const auto &ar0) {
+    using A0 = std::decay_t<decltype(ar0)>;
+    constexpr bool F = std::is_same<A0, ArF64>::value;
+    constexpr bool W8 = LTW && ALLF;  // ALLF: A0 is ArF64
+    if constexpr (W8) {
+      RowTw<LOGN2>::template stage<true>(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
+      RowTw<LOGN2>::template stage<true>(rtw + RowTw<LOGN2>::ENTRIES, (const uint64_t *)ar0.itw, n1 + row0,
+                                         threadIdx.x, 256 * QN);
+      __syncthreads();
+    } else if constexpr (LTW) {
+      RowTw<LOGN2>::stage(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
+      __syncthreads();
+    }
+    const auto ar = [&] {
+      if constexpr (LTW)
+        return row_policy<LOGN2, W8>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
+                                     W8 ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
+      else
+        return ar0;
+    }();
+    using A = std::decay_t<decltype(ar)>;
+    using V = typename A::V;
+    for (; p < pb1; p += QN) {
+      const unsigned pn = p + QN;
+      // f: FP64 accumulators (|.| < 3 q before each fold); a: integer lazy ones
+      V f0[8], f1[8];
+      uint64_t a0[8], a1[8];
+      if (nx == 0)  // one-digit keys: a q slot has no converted limb
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          f0[k] = f1[k] = 0;
+          a0[k] = a1[k] = 0;
+        }
+#pragma unroll
+      for (int u = 0; u < NX; u++) {
+        if (u >= nx)
+          continue;
+        const unsigned j = jof(u);
+        V r[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          r[k] = A::load(xn[u][k]);
+        if (pn < pb1)
+          fetch(xn[u], j, pn);  // next pair's tile, in flight meanwhile
+        wave_sync();            // the previous phase has finished with the LDS tile
+        rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
+        if constexpr (F) {
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
+            const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
+            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
+            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
+            f0[k] = u ? f0[k] + tb : tb;
+            f1[k] = u ? f1[k] + ta : ta;
+            if (u == 1) {  // two products (< 3 q): fold before the next term
+              f0[k] = f64_red(f0[k], ar.q, ar.qinv);
+              f1[k] = f64_red(f1[k], ar.q, ar.qinv);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const uint64_t v = ar.canon(r[k]);
+            if (u == 0)
+              a0[k] = a1[k] = 0;
+            mac_i(a0[k], v, kl[2 * j][256 * k + th]);
+            mac_i(a1[k], v, kl[2 * j + 1][256 * k + th]);
+          }
+        }
+      }
+      if (jo < NDIG) {
+        // q limb: own digit x = a1 b1 (the NTT-form d2 limb) and P (d0, d1),
+        // from the four input words at this thread's natural positions 8 th + k
+        const size_t off = p * d01.in_stride + ((size_t)t << logn) + toff + 8 * th;
+        const uint64_t *pa = d01.a + off, *pb = d01.b + off;
+        if constexpr (F) {
+          const double Pd = f64_from_u52(mc.pmod), Pq = Pd * ar.qinv;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            double A0[4], A1[4], B0[4], B1[4];
+            auto ld4 = [&](const uint64_t *s, double (&x)[4]) {
+              const ulonglong2 *v2 = (const ulonglong2 *)(s + 4 * h);
+              const ulonglong2 w0 = v2[0], w1 = v2[1];
+              x[0] = f64_from_u52(w0.x);
+              x[1] = f64_from_u52(w0.y);
+              x[2] = f64_from_u52(w1.x);
+              x[3] = f64_from_u52(w1.y);
+            };
+            ld4(pa, A0);
+            ld4(pb, B0);
+            ld4(pa + d01.in_pstride, A1);
+            ld4(pb + d01.in_pstride, B1);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const int k = 4 * h + e;
+              const double eb = __longlong_as_double((long long)kl[2 * jo][256 * k + th]);
+              const double ea = __longlong_as_double((long long)kl[2 * jo + 1][256 * k + th]);
+              const double x = f64_mulmod(A1[e], B1[e], B1[e] * ar.qinv, ar.q);  // |x| < 1.5 q
+              const double d0 = f64_mulmod(A0[e], B0[e], B0[e] * ar.qinv, ar.q);
+              const double d1 = f64_red(f64_mulmod(A0[e], B1[e], B1[e] * ar.qinv, ar.q) +
+                                            f64_mulmod(A1[e], B0[e], B0[e] * ar.qinv, ar.q),
+                                        ar.q, ar.qinv);
+              // |f| <= q/2 + 1.5 q after the fold, then + two products < 1.5 q
+              const double g0 = f64_red(f0[k], ar.q, ar.qinv) + f64_mulmod(x, eb, eb * ar.qinv, ar.q);
+              const double g1 = f64_red(f1[k], ar.q, ar.qinv) + f64_mulmod(x, ea, ea * ar.qinv, ar.q);
+              f0[k] = f64_red(g0, ar.q, ar.qinv) + f64_mulmod(d0, Pd, Pq, ar.q);
+              f1[k] = f64_red(g1, ar.q, ar.qinv) + f64_mulmod(d1, Pd, Pq, ar.q);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            uint64_t A0[4], A1[4], B0[4], B1[4];
+            auto ld4 = [&](const uint64_t *s, uint64_t (&x)[4]) {
+              const ulonglong2 *v2 = (const ulonglong2 *)(s + 4 * h);
+              const ulonglong2 w0 = v2[0], w1 = v2[1];
+              x[0] = w0.x;
+              x[1] = w0.y;
+              x[2] = w1.x;
+              x[3] = w1.y;
+            };
+            ld4(pa, A0);
+            ld4(pb, B0);
+            ld4(pa + d01.in_pstride, A1);
+            ld4(pb + d01.in_pstride, B1);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const int k = 4 * h + e;
+              mac_i(a0[k], mul_mod(A1[e], B1[e], mc), kl[2 * jo][256 * k + th]);
+              mac_i(a1[k], mul_mod(A1[e], B1[e], mc), kl[2 * jo + 1][256 * k + th]);
+              const uint64_t d0 = mul_mod(A0[e], B0[e], mc);
+              const uint64_t d1 = add_mod(mul_mod(A0[e], B1[e], mc), mul_mod(A1[e], B0[e], mc), q);
+              const uint64_t c0 = a0[k] >= q ? a0[k] - q : a0[k], c1 = a1[k] >= q ? a1[k] - q : a1[k];
+              a0[k] = add_mod(c0, mul_shoup(d0, mc.pmod, mc.pmodp, q), q);
+              a1[k] = add_mod(c1, mul_shoup(d1, mc.pmod, mc.pmodp, q), q);
+            }
+          }
+        }
+      } else if constexpr (!F) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          a0[k] = a0[k] >= q ? a0[k] - q : a0[k];
+          a1[k] = a1[k] >= q ? a1[k] - q : a1[k];
+        }
+      }
+      // (f0, f1) / (a0, a1): this thread's words 8 th + k of slot t (natural order)
+      if constexpr (KEEP) {
+        const uint64_t di = dinv[t], dip = dinvp[t];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          const unsigned poly = 2 * p + half;
+          const uint64_t *cv = conv + (((size_t)poly * t_n + t) << logn) + toff;
+          V r[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            r[k] = A::load(cv[(row << LOGN2) + l + T::TA * k]);
+          wave_sync();
+          rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
+          uint64_t o[8];
+          if constexpr (F) {
+            const double dd = f64_from_u52(di), dq = dd * ar.qinv;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+              const double x = f64_red(half ? f1[k] : f0[k], ar.q, ar.qinv);  // |x - c| < 2.5 q
+              o[k] = ar.canon(f64_mulmod(x - r[k], dd, dq, ar.q));
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+              o[k] = mul_shoup(sub_mod(half ? a1[k] : a0[k], ar.canon(r[k]), q), di, dip, q);
+          }
+          ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + 8 * th);
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            d2[i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          V r[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            if constexpr (F)
+              r[k] = f64_red(half ? f1[k] : f0[k], ar.q, ar.qinv);
+            else
+              r[k] = A::load(half ? a1[k] : a0[k]);
+          }
+          wave_sync();
+          rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
+          uint64_t *o = dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            o[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+        }
+      }
+    }
+  });
+}
+
+template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW>
+static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
+                       size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl,
+                       unsigned nm, unsigned t_lo, unsigned t_n)
+{
+  const unsigned n = G.n, groups = t_n * (n / 2048);
+  // pair ranges of about 3 pairs per quarter; more, shorter ranges while the
+  // grid would not give every CU two workgroups
+  const unsigned per = 3 * QN;
+  unsigned members = std::max(1u, (count + per - 1) / per);
+  while (members < count && (size_t)groups * members < 2 * 256)
+    members++;
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  const size_t t1_stride = (size_t)NDIG * nm * n;
+  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, LTW>;
+  hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, T1, t1_stride, d01, evkm,
+                     dst, dst_pstride, conv, dinv, dinvp, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
+                     members, t_lo, t_n, tw, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int LOGN2>
+static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
+                         const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv,
+                         const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo,
+                         unsigned t_n)
+{
+  // LDS: the key tile (2 ndig x 16 KB) + 16 KB per quarter stream (+ 32 KB of
+  // row twiddles where they fit) <= 160 KB
+  switch (ndig) {
+  case 1:
+    ksq_launch<LOGN2, 1, 4, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    break;
+  case 2:
+    if (allf)
+      ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    else
+      ksq_launch<LOGN2, 2, 3, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo,
+                                     t_n);
+    break;
+  default: gpqhe_die("split key switch: %u digits", ndig);
+  }
+}
+
+void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
+             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv,
+             const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
+{
+#ifdef KSQ_DEV  // analysis builds: the bench's instantiations only
+  if (logn2 == 8 && ndig == 2 && allf) {
+    ksq_launch<8, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    return;
+  }
+  gpqhe_die("KSQ_DEV build");
+#else
+  switch (logn2) {
+  case 7: ksq_dispatch<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  case 8: ksq_dispatch<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  case 9: ksq_dispatch<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  default: gpqhe_die("split key switch: row length 2^%u", logn2);
+  }
+#endif
+}

@@ -1,0 +1,790 @@
+// ntt_device.h - device building blocks shared by the gfx950 kernel files:
+// modular / FP64 arithmetic policies, the 4-step NTT column and row passes on
+// LDS tiles, and the XCD-aware block mapping.
+#pragma once
+
+#include "gpqhe_internal.h"
+
+#include <type_traits>
+
+// ===========================================================================
+// NTT v2 (two-pass, n = 2^13 .. 2^16): 4096-element tiles, 256 threads,
+// Harvey lazy butterflies (values in [0, 4q) inside a pass, canonical at every
+// pass boundary), interleaved (w, w') twiddle pairs (one 16-byte load), round
+// A loaded straight from HBM into registers, prime-major workgroup order so
+// the workgroups resident at one time share one prime's twiddle table.
+// ===========================================================================
+struct Tw2 {
+  const uint64_t *fwd;  // [nmod][n][2] (w, floor(w 2^64 / q))
+  const uint64_t *inv;
+  const double *fwdd;   // [nmod][n][2] (w, w / q) as doubles (moduli < 2^51)
+  const double *invd;
+};
+
+__device__ __forceinline__ uint64_t lazy_lt2q(uint64_t x, uint64_t q2)
+{
+  return x >= q2 ? x - q2 : x;
+}
+
+__device__ __forceinline__ uint64_t canon4(uint64_t x, uint64_t q, uint64_t q2)
+{
+  x = x >= q2 ? x - q2 : x;
+  return x >= q ? x - q : x;
+}
+
+// forward CT stages on E = 2^LE registers; twiddle run of stage s starts at
+// bb >> (log_thi - s + 1); inputs < 4q, outputs < 4q
+template <int LE>
+__device__ __forceinline__ void fwd_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
+                                           int log_thi, uint64_t q)
+{
+  constexpr int E = 1 << LE;
+  const uint64_t q2 = 2 * q;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_thi - s + 1);
+    const int half = E >> (s + 1);
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
+      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
+      const uint64_t U = lazy_lt2q(x[k], q2);
+      const uint64_t V = mul_shoup_lazy(x[k + half], w, wp, q);
+      x[k] = U + V;
+      x[k + half] = U - V + q2;
+    }
+  }
+}
+
+// inverse GS stages; inputs < 2q, outputs < 2q
+template <int LE>
+__device__ __forceinline__ void inv_stages(uint64_t (&x)[1 << LE], const uint64_t *__restrict__ tw2, uint64_t bb,
+                                           int log_tlo, uint64_t q)
+{
+  constexpr int E = 1 << LE;
+  const uint64_t q2 = 2 * q;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_tlo + s + 1);
+    const int half = 1 << s;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
+      const uint64_t w = tw2[i2], wp = tw2[i2 + 1];
+      const uint64_t U = x[k], V = x[k + half];
+      x[k] = lazy_lt2q(U + V, q2);
+      x[k + half] = mul_shoup_lazy(U - V + q2, w, wp, q);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FP64 butterflies for moduli q < 2^51 (the FP64 pipe is full rate on gfx950
+// and twice as fast as 64-bit integer Shoup per butterfly, scripts/ubench_bfly).
+// Values are signed doubles holding exact integers:
+//   mulmod: h = fl(y w), l = fma(y, w, -h) (exact), qt = rint(y fl(w/q)),
+//           T = fma(-qt, q, h) + l = y w - qt q exactly.  The quotient error
+//           is below 1/2 + |y| 2^-52, so for |y| <= 2q < 2^52 |T| < 1.5 q.
+//   red:    x - rint(x fl(1/q)) q, |result| <= q/2 (+ negligible).
+// CT: X = red(x[k]), T = mulmod(x[k+h]); outputs X +- T, |.| < 2q.
+// GS: outputs red(U + V) and mulmod(U - V) with |U - V| < 2q.
+// Every intermediate is an integer below 2^53, so the residues are exact and
+// the canonical outputs equal the integer path's bit for bit.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double f64_mulmod(double y, double w, double wq, double q)
+{
+  const double h = y * w;
+  const double l = __fma_rn(y, w, -h);
+  const double qt = rint(y * wq);
+  return __fma_rn(-qt, q, h) + l;
+}
+
+__device__ __forceinline__ double f64_red(double x, double q, double qinv)
+{
+  return __fma_rn(-rint(x * qinv), q, x);
+}
+
+// u64 <-> f64 for integers below 2^52 without the generic conversions (4 and
+// ~7 instructions): 2^52 + x has x as its mantissa bits.
+__device__ __forceinline__ double f64_from_u52(uint64_t x)
+{
+  return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 0x1p52;
+}
+
+// canonical residue of x (integer, |x| < 2^53): reduce, lift negatives by
+// q and read the mantissa of 2^52 + v
+__device__ __forceinline__ uint64_t f64_canon(double x, double q, double qinv)
+{
+  const double v = f64_red(x, q, qinv);
+  const double b = v < 0 ? q + 0x1p52 : 0x1p52;
+  return (uint64_t)__double_as_longlong(v + b) & ((1ull << 52) - 1);
+}
+
+template <int LE>
+__device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
+                                             int log_thi, double q, double qinv)
+{
+  constexpr int E = 1 << LE;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_thi - s + 1);
+    const int half = E >> (s + 1);
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
+      const double X = f64_red(x[k], q, qinv);
+      const double T = f64_mulmod(x[k + half], twd[i2], twd[i2 + 1], q);
+      x[k] = X + T;
+      x[k + half] = X - T;
+    }
+  }
+}
+
+template <int LE>
+__device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
+                                             int log_tlo, double q, double qinv)
+{
+  constexpr int E = 1 << LE;
+#pragma unroll
+  for (int s = 0; s < LE; s++) {
+    const uint64_t Bs = bb >> (log_tlo + s + 1);
+    const int half = 1 << s;
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      if (k & half)
+        continue;
+      const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
+      const double U = x[k], V = x[k + half];
+      x[k] = f64_red(U + V, q, qinv);
+      x[k + half] = f64_mulmod(U - V, twd[i2], twd[i2 + 1], q);
+    }
+  }
+}
+
+// Arithmetic policies: the NTT kernels are written once against these.  Both
+// read and write canonical u64 residues; ArF64 requires q < 2^51.
+struct ArInt {
+  using V = uint64_t;
+  uint64_t q;
+  const uint64_t *tw;   // this modulus' forward (w, w') pairs
+  const uint64_t *itw;  // and inverse
+  __device__ static V load(uint64_t x) { return x; }
+  __device__ uint64_t canon(V x) const { return canon4(x, q, 2 * q); }  // x < 4q
+  __device__ static uint64_t bits(V x) { return x; }
+  __device__ static V unbits(uint64_t b) { return b; }
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const { fwd_stages<LE>(x, tw, bb, log_thi, q); }
+  template <int LE>
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const { inv_stages<LE>(x, itw, bb, log_tlo, q); }
+  // canonical x w for a constant w < q (Shoup pair)
+  __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
+  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t wp) const { return mulc(x, w, wp); }  // (FP64 only)
+};
+
+struct ArF64 {
+  using V = double;
+  double q, qinv;
+  const double *tw;   // this modulus' forward (w, w / q) pairs
+  const double *itw;  // and inverse
+  __device__ static V load(uint64_t x) { return f64_from_u52(x); }  // x canonical (< q)
+  __device__ uint64_t canon(V x) const { return f64_canon(x, q, qinv); }
+  __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
+  __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv);
+  }
+  template <int LE>
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  {
+    inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv);
+  }
+  __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
+  {
+    const double wd = f64_from_u52(w);
+    return canon(f64_mulmod(x, wd, wd / q, q));
+  }
+  // x w as the bits of a canonical double in [0, q) (FP64 basis conversion input)
+  __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t) const
+  {
+    const double wd = f64_from_u52(w);
+    const double v = f64_red(f64_mulmod(x, wd, wd / q, q), q, qinv);
+    return (uint64_t)__double_as_longlong(v < 0 ? v + q : v);
+  }
+};
+
+// FP64 fast basis conversion term y c mod q_t for canonical y < q_i < 2^51 and
+// a constant c < q_t < 2^51 with cq = fl(c / q_t): y c / q_t < 2^51, so the
+// quotient estimate is off by at most 1, |result| <= q_t and every
+// intermediate is an integer below 2^53 (exact).  Sums of up to three terms
+// stay below 2^53; longer sums are reduced in between (f64_red).
+__device__ __forceinline__ double fbc_term(double y, double c, double cq, double q)
+{
+  return f64_mulmod(y, c, cq, q);
+}
+
+constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
+
+// Forward row passes with the twiddles of one row tile staged in LDS.  A
+// 2^LOGN2-point row pass of global row rho uses, at its stage of level lam
+// (0 .. LOGN2-1), the 2^lam twiddles tw[rho 2^lam + g]; the R rows
+// [rho0, rho0 + R) of a tile need R 2^lam consecutive entries per level,
+// stored at R (2^lam - 1) (R (2^LOGN2 - 1) 16-byte entries in all, ~32 KB).
+// A stage whose run starts at Bs = bb >> shift is at level LOGN2 - shift.
+template <int LOGN2>
+struct RowTw {
+  static constexpr int R = 2048 >> LOGN2, ENTRIES = R * ((1 << LOGN2) - 1);
+  const uint64_t *lds;  // ENTRIES x 2 words
+  int64_t rel;          // R - rho0
+  __device__ __forceinline__ uint64_t idx(uint64_t i, int shift) const
+  {
+    return (uint64_t)((int64_t)i + (rel << (LOGN2 - shift)) - R);
+  }
+  // copy the tile's entries of a [n][2] table (16-byte entries) into lds; W8:
+  // only the first word of each (8-byte entries: FP64 w, w / q recomputed)
+  template <bool W8 = false>
+  static __device__ __forceinline__ void stage(uint64_t *dst, const uint64_t *tab, unsigned rho0, unsigned tid,
+                                               unsigned nthreads)
+  {
+    for (unsigned e = tid; e < (unsigned)ENTRIES; e += nthreads) {
+      const unsigned lam = 31 - __clz(e / R + 1);  // level of entry e: R (2^lam - 1) <= e
+      const unsigned g = e - R * ((1u << lam) - 1);
+      const size_t src = ((size_t)rho0 << lam) + g;
+      if (W8)
+        dst[e] = tab[2 * src];
+      else
+        ((ulonglong2 *)dst)[e] = ((const ulonglong2 *)tab)[src];
+    }
+  }
+};
+
+// ArF64 / ArInt with the forward twiddles from a RowTw table (the inverse
+// stays on the global table).  ArF64Row<.., true>: 8-byte entries (w only;
+// w / q recomputed as w fl(1/q), which moves the quotient estimate by at most
+// one and so never a canonical result) for both directions (itl: inverse).
+template <int LOGN2, bool W8 = false>
+struct ArF64Row : ArF64 {
+  RowTw<LOGN2> rt;
+  const uint64_t *itl = nullptr;
+  __device__ __forceinline__ double2 twf(const uint64_t *tab, uint64_t e) const
+  {
+    if constexpr (W8) {
+      const double w = __longlong_as_double((long long)tab[e]);
+      return make_double2(w, w * qinv);
+    } else {
+      return ((const double2 *)tab)[e];
+    }
+  }
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    constexpr int E = 1 << LE;
+#pragma unroll
+    for (int s = 0; s < LE; s++) {
+      const int shift = log_thi - s + 1;
+      const uint64_t Bs = bb >> shift;
+      const int half = E >> (s + 1);
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if (k & half)
+          continue;
+        const double2 w = twf(rt.lds, rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift));
+        const double X = f64_red(x[k], q, qinv);
+        const double T = f64_mulmod(x[k + half], w.x, w.y, q);
+        x[k] = X + T;
+        x[k + half] = X - T;
+      }
+    }
+  }
+  template <int LE>
+  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  {
+    if constexpr (!W8) {
+      ArF64::inv<LE>(x, bb, log_tlo);
+    } else {
+      constexpr int E = 1 << LE;
+#pragma unroll
+      for (int s = 0; s < LE; s++) {
+        const int shift = log_tlo + s + 1;
+        const uint64_t Bs = bb >> shift;
+        const int half = 1 << s;
+#pragma unroll
+        for (int k = 0; k < E; k++) {
+          if (k & half)
+            continue;
+          const double2 w = twf(itl, rt.idx(Bs + (uint64_t)(k >> (s + 1)), shift));
+          const double U = x[k], V_ = x[k + half];
+          x[k] = f64_red(U + V_, q, qinv);
+          x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
+        }
+      }
+    }
+  }
+};
+
+template <int LOGN2>
+struct ArIntRow : ArInt {
+  RowTw<LOGN2> rt;
+  template <int LE>
+  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    constexpr int E = 1 << LE;
+    const uint64_t q2 = 2 * q;
+#pragma unroll
+    for (int s = 0; s < LE; s++) {
+      const int shift = log_thi - s + 1;
+      const uint64_t Bs = bb >> shift;
+      const int half = E >> (s + 1);
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if (k & half)
+          continue;
+        const uint64_t e = rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift);
+        const ulonglong2 w = ((const ulonglong2 *)rt.lds)[e];
+        const uint64_t U = lazy_lt2q(x[k], q2);
+        const uint64_t V_ = mul_shoup_lazy(x[k + half], w.x, w.y, q);
+        x[k] = U + V_;
+        x[k + half] = U - V_ + q2;
+      }
+    }
+  }
+};
+
+template <int LOGN2, bool W8 = false>
+__device__ __forceinline__ ArF64Row<LOGN2, W8> row_policy(const ArF64 &a, const uint64_t *lds, int64_t rel,
+                                                          const uint64_t *ilds = nullptr)
+{
+  ArF64Row<LOGN2, W8> r;
+  static_cast<ArF64 &>(r) = a;
+  r.rt = RowTw<LOGN2>{lds, rel};
+  r.itl = ilds;
+  return r;
+}
+
+template <int LOGN2, bool W8 = false>
+__device__ __forceinline__ ArIntRow<LOGN2> row_policy(const ArInt &a, const uint64_t *lds, int64_t rel,
+                                                      const uint64_t * = nullptr)
+{
+  static_assert(!W8, "integer twiddles need their Shoup companions");
+  ArIntRow<LOGN2> r;
+  static_cast<ArInt &>(r) = a;
+  r.rt = RowTw<LOGN2>{lds, rel};
+  return r;
+}
+
+// Run f with the arithmetic policy of modulus index m (q = its prime).
+template <class F>
+__device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
+{
+  const size_t o = (size_t)m << (logn + 1);
+  if (q < F64_QMAX && tw.fwdd)
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+  else
+    f(ArInt{q, tw.fwd + o, tw.inv + o});
+}
+
+// FP64 basis conversion (fbc_term) where it measured faster than the 128-bit
+// integer sums + REDC (same box, per 64-pair chunk at N=2^16, L=8): the INVC
+// ks_cols4 (323 vs 388 us) and dn_cols (296 vs 309 us).  The NT = 4 ks_cols4
+// (config 5) keeps the integer sums (308 vs 488 us with FP64).  Both forms are
+// exact, so the choice never changes a bit.
+constexpr bool FBC64_KS_INVC = true, FBC64_DN = true, FBC64_KS_NT4 = false;
+
+// with_arith for kernels instantiated per prime set: ALL_F64 (every modulus
+// < 2^51, FP64 tables present) keeps only the FP64 policy in the code.
+template <bool ALL_F64, class F>
+__device__ __forceinline__ void with_arith_t(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
+{
+  if constexpr (ALL_F64) {
+    const size_t o = (size_t)m << (logn + 1);
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+  } else {
+    with_arith(q, m, logn, tw, f);
+  }
+}
+
+// Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
+// B reads 16 consecutive columns per thread at a 16-column lane stride; the
+// XOR spreads those lanes over distinct banks (8-way conflict without it).
+__device__ __forceinline__ int rswz(int c)
+{
+  return c ^ ((c >> 4) & 15);
+}
+
+// block -> (limb, tile) in prime-major order: all tiles of all limbs that use
+// basis slot t run before slot t + 1.
+__device__ __forceinline__ void pm_decode(const LimbSet &s, unsigned tiles, unsigned &v, unsigned &tile)
+{
+  const unsigned groups = s.count / s.per;
+  const unsigned b = blockIdx.x;
+  const unsigned t = b / (groups * tiles);
+  const unsigned rem = b - t * groups * tiles;
+  const unsigned grp = rem / tiles;
+  tile = rem - grp * tiles;
+  v = grp * s.per + t;
+}
+
+// Column pass: tile = T rows x C columns (T C = 4096).
+template <int LOGT, bool INV, class A>
+__device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64_t *y, unsigned n2, uint64_t *lds,
+                                          uint64_t sw, uint64_t swp)
+{
+  using V = typename A::V;
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1;
+  const int t = threadIdx.x;
+  if constexpr (!INV) {
+    // round A: rows l + 16 k (distances T/2 .. 16)
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      const unsigned vo = (unsigned)l * n2 + c;  // 32-bit per-thread offset, uniform row bases
+      V r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = A::load((x + (size_t)(16 * k) * n2)[vo]);
+      ar.template fwd<LEA>(r, T, LOGT - 1);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        lds[(l + 16 * k) * CP + c] = A::bits(r[k]);
+    }
+    __syncthreads();
+    // round B: rows 16 g + k (distances 8 .. 1)
+    const int c = t % C, g = t / C;
+    const unsigned vo = (unsigned)(16 * g) * n2 + c;
+    V r[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      r[k] = A::unbits(lds[(16 * g + k) * CP + c]);
+    ar.template fwd<4>(r, T + 16 * g, 3);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      (y + (size_t)k * n2)[vo] = ar.canon(r[k]);
+  } else {
+    {
+      const int c = t % C, g = t / C;
+      const unsigned vo = (unsigned)(16 * g) * n2 + c;
+      V r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        r[k] = A::load((x + (size_t)k * n2)[vo]);
+      ar.template inv<4>(r, T + 16 * g, 0);
+#pragma unroll
+      for (int k = 0; k < 16; k++)
+        lds[(16 * g + k) * CP + c] = A::bits(r[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < C / 16; it++) {
+      const int item = t + 256 * it, c = item % C, l = item / C;
+      const unsigned vo = (unsigned)l * n2 + c;
+      V r[EA];
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        r[k] = A::unbits(lds[(l + 16 * k) * CP + c]);
+      ar.template inv<LEA>(r, T, 4);
+#pragma unroll
+      for (int k = 0; k < EA; k++)
+        (y + (size_t)(16 * k) * n2)[vo] = ar.mulc(r[k], sw, swp);
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Row pass, 8 elements per thread: tile = R x N2 with R N2 = 2048 (16 KiB of
+// LDS, no padding), three register rounds of 3, 3 and LOGN2 - 6 stages.
+// Half the registers of the 16-element form, so twice the waves per CU to
+// overlap one block's butterflies with another's loads.
+//   round A: thread (row, l < TA = N2/8)    elements l + TA k
+//   round B: thread (row, m < 8, l' < TA/8) elements m TA + l' + (TA/8) k
+//   round C: thread (row, h < TA)           elements 8 h + k (consecutive)
+// LDS swizzle (conflict-free for all four access patterns, checked offline):
+// column c of row r sits at c ^ ((c >> 3) & (TA - 1)) (^ (r & 1) << 4 for
+// N2 = 128).
+// ---------------------------------------------------------------------------
+// Every exchange of the 8-element row passes stays inside one row, and a
+// row belongs to one wave (TA = N2 / 8 threads per row, 64 / TA rows per
+// wave), so the row passes synchronise per wave, not per block: LDS
+// operations of one wave execute in order, the fences only keep the compiler
+// from moving them across the exchange.  Waves of a block never wait for each
+// other.
+__device__ __forceinline__ void wave_sync()
+{
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Word i < 8 of this thread in a wave-local coalesced walk over a
+// 2048-element row tile: wave w covers elements [512 w, 512 w + 512), which
+// are exactly its own rows.
+__device__ __forceinline__ int wl_elem(int i)
+{
+  return (threadIdx.x & ~63) * 8 + (threadIdx.x & 63) + 64 * i;
+}
+
+template <int LOGN2>
+struct Row8 {
+  static constexpr int N2 = 1 << LOGN2, R = 2048 / N2, TA = N2 / 8, TB = TA / 8, EC = 1 << (LOGN2 - 6);
+  // LDS layout: one pad word per 8 (row stride RS = 9 N2 / 8).  Column c of
+  // a row sits at c + c / 8, so every per-thread element set of rounds A, B, C
+  // and of the coalesced transposes is one base plus compile-time offsets
+  // (one address VGPR per round, not one per element), and all of them are
+  // conflict-free for ds_read_b64 except two-way on 3 banks in round A.
+  static constexpr int RS = N2 + N2 / 8, WORDS = R * RS;
+  static __device__ __forceinline__ int padc(int c) { return c + (c >> 3); }
+  static __device__ __forceinline__ int at(int row, int c) { return row * RS + padc(c); }
+  // column c0 + d with (c0 & 7) + (d & 7) < 8: base + constant
+  static __device__ __forceinline__ int at2(int row, int c0, int d) { return row * RS + padc(c0) + padc(d); }
+  // word wl_elem(i) of local thread th (wave-local coalesced walk)
+  static __device__ __forceinline__ int wl(int th, int i)
+  {
+    const int e0 = (th & ~63) * 8;  // the wave's first element: a row start
+    return (e0 >> LOGN2) * RS + ((64 * i) >> LOGN2) * RS + padc(th & 63) + padc((64 * i) & (N2 - 1));
+  }
+};
+
+// forward row pass of one tile, rounds A..C: round A input in r (the
+// thread's A elements), canonical result in out (the thread's C elements)
+// forward row pass of one tile leaving the thread's C elements lazy in r
+// (|.| < 2q for ArF64, < 4q for ArInt)
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0,
+                                              const int th = (int)threadIdx.x)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int l = th % T::TA;
+    ar.template fwd<3>(r, rb, LOGN2 - 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, l, T::TA * k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::unbits(lds[T::at2(row, c0, T::TB * k)]);
+    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, c0, T::TB * k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  const int h = th % T::TA;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = A::unbits(lds[T::at2(row, 8 * h, k)]);
+#pragma unroll
+  for (int j = 0; j < 8 / T::EC; j++) {
+    V g[T::EC];
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      g[e] = r[j * T::EC + e];
+    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      r[j * T::EC + e] = g[e];
+  }
+}
+
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)[8], uint64_t *lds, const A &ar,
+                                          uint64_t rowbase0)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int th = threadIdx.x, row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int l = th % T::TA;
+    ar.template fwd<3>(r, rb, LOGN2 - 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, l, T::TA * k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::unbits(lds[T::at2(row, c0, T::TB * k)]);
+    ar.template fwd<3>(r, rb + mb * T::TA, LOGN2 - 4);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, c0, T::TB * k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  const int h = th % T::TA;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = A::unbits(lds[T::at2(row, 8 * h, k)]);
+#pragma unroll
+  for (int j = 0; j < 8 / T::EC; j++) {
+    V g[T::EC];
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      g[e] = r[j * T::EC + e];
+    ar.template fwd<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, LOGN2 - 7);
+#pragma unroll
+    for (int e = 0; e < T::EC; e++)
+      out[j * T::EC + e] = ar.canon(g[e]);
+  }
+}
+
+// inverse row pass of one tile: input r = thread's C elements (canonical or
+// bounded as the policy's inverse allows), result r = thread's A elements
+// (lazy; canonicalise with ar.canon)
+template <int LOGN2, class A>
+__device__ __forceinline__ void rows8_inv(typename A::V (&r)[8], uint64_t *lds, const A &ar, uint64_t rowbase0,
+                                          const int th = (int)threadIdx.x)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int row = th / T::TA;
+  const uint64_t rb = (rowbase0 + row) << LOGN2;
+  {
+    const int h = th % T::TA;
+#pragma unroll
+    for (int j = 0; j < 8 / T::EC; j++) {
+      V g[T::EC];
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        g[e] = r[j * T::EC + e];
+      ar.template inv<LOGN2 - 6>(g, rb + 8 * h + T::EC * j, 0);
+#pragma unroll
+      for (int e = 0; e < T::EC; e++)
+        r[j * T::EC + e] = g[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, 8 * h, k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  {
+    const int mb = (th % T::TA) / T::TB, l2 = th % T::TB, c0 = mb * T::TA + l2;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::unbits(lds[T::at2(row, c0, T::TB * k)]);
+    ar.template inv<3>(r, rb + mb * T::TA, LOGN2 - 6);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, c0, T::TB * k)] = A::bits(r[k]);
+  }
+  wave_sync();
+  {
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::unbits(lds[T::at2(row, l, T::TA * k)]);
+    ar.template inv<3>(r, rb, LOGN2 - 3);
+  }
+}
+
+// Inverse row pass of one tile whose words the thread already holds in the
+// wave-local coalesced order (raw[i] = word wl_elem(i)).
+template <int LOGN2, bool INV, class A>
+__device__ __forceinline__ void rows8_tile_raw(const A &ar, const uint64_t (&raw)[8], uint64_t *y, uint64_t *lds,
+                                               uint64_t rowbase0)
+{
+  static_assert(INV, "forward tiles load their own words");
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int th = threadIdx.x, row = th / T::TA, h = th % T::TA, l = th % T::TA;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    lds[T::wl(th, i)] = raw[i];
+  wave_sync();
+  V r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = A::load(lds[T::at2(row, 8 * h, k)]);
+  wave_sync();
+  rows8_inv<LOGN2>(r, lds, ar, rowbase0);
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+}
+
+template <int LOGN2, bool INV, class A>
+__device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint64_t *y, uint64_t *lds,
+                                           uint64_t rowbase0)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int th = threadIdx.x, row = th / T::TA;
+  V r[8];
+  if constexpr (!INV) {
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+    uint64_t out[8];
+    rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0);
+    const int h = th % T::TA;
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, 8 * h, k)] = out[k];
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      y[wl_elem(i)] = lds[T::wl(th, i)];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      lds[T::wl(th, i)] = x[wl_elem(i)];
+    wave_sync();
+    const int h = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::load(lds[T::at2(row, 8 * h, k)]);
+    wave_sync();
+    rows8_inv<LOGN2>(r, lds, ar, rowbase0);
+    const int l = th % T::TA;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+  }
+}
+
+
+__device__ __forceinline__ unsigned basis_mod(unsigned t, unsigned lvl, unsigned L)
+{
+  return t < lvl ? t : L + (t - lvl);
+}
+
+// XCD-aware grouping: workgroups are dealt round-robin over the 8 XCDs, so
+// blocks b and b + 8 share one XCD's L2.  Map block b to (group g, member i)
+// such that the `members` blocks of a group share b % 8 and are dispatched
+// close together; groups are padded to a multiple of 8 (extra blocks exit).
+// Placement only affects speed, never correctness.
+__device__ __forceinline__ bool xcd_group(unsigned members, unsigned ngroups, unsigned &g, unsigned &i)
+{
+  const unsigned b = blockIdx.x, x = b & 7, s = b >> 3;
+  i = s % members;
+  g = (s / members) * 8 + x;
+  return g < ngroups;
+}
+
+static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
+{
+  return ((ngroups + 7) / 8) * 8 * members;
+}
+
+// Split key switch, kept / dropped basis slots (ks_split.hip): one launch of
+// ksq_kernel for row length 2^logn2 and ndig digits.
+void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
+             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv,
+             const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n);

@@ -1,19 +1,28 @@
-"""Summarise gpurun_out/<run>/bench_*.log files: value and top kernels."""
+"""Summarise bench logs (a gpurun_out/<run> directory or log files): value,
+60-bit / config-5 values and the per-kernel table."""
 import glob
 import json
+import os
 import sys
 
-for f in sorted(glob.glob(f"gpurun_out/{sys.argv[1]}/bench_*.log")):
+files = []
+for a in sys.argv[1:]:
+    files += sorted(glob.glob(os.path.join(a, "bench_*.log"))) if os.path.isdir(a) else [a]
+for f in files:
     line = [l for l in open(f) if l.startswith('{"metric"')]
     if not line:
         print(f, "NO RESULT")
         continue
-    d = json.loads(line[0])
+    d = json.loads(line[-1])
     ks = sorted(d.get("kernels", {}).items(), key=lambda kv: -kv[1]["share"])
-    print(f"{f.split('/')[-1]:24s} {d['value']:9.0f} {d['unit']}  dom={d['roofline']['kernel']} "
-          f"{d['roofline']['achieved']:.0f} GB/s")
+    extra = ""
+    if "value_60bit" in d:
+        extra += f"  60-bit {d['value_60bit']:.0f}"
+    if "config5" in d:
+        extra += f"  c5 {d['config5']['value']:.0f}"
+    print(f"{os.path.basename(f):16s} {d['value']:9.0f} {d['unit']}{extra}  ms/step {d['ms_per_step']:.3f}")
     if "ntt_roundtrip" in d:
         t = d["ntt_roundtrip"]
         print(f"    ntt roundtrip {t['polys']} polys: {t['roundtrip_ms']:.2f} ms, {t['alg_GBs']:.0f} GB/s")
     for k, v in ks:
-        print(f"    {k:28s} {v['avg_us']:8.1f} us  {v['share']*100:5.1f}%  {v['streamed_GBs']:7.0f} GB/s")
+        print(f"    {k:28s} {v['launches']:5d} x {v['avg_us']:8.1f} us  {v['share']*100:5.1f}%  {v['streamed_GBs']:7.0f} GB/s")

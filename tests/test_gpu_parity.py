@@ -207,7 +207,7 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 through the streaming inner
     product, the bench's dnum=2/K=4 with 60-bit and with < 2^51 primes), the
     config 5 op at n=2^17, L=12, and the other fused tilings, on 3
-    random-residue pairs (one ks_rows2 run per pair)."""
+    random-residue pairs (one pair per quarter stream of the split key switch)."""
     want, got = mul_batch_both(oracle, product, name, 3)
     assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
 
@@ -216,11 +216,13 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
                                             ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None)])
 def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
     """The headline shape (bench.py): n=2^16, L=8,
-    dnum=2, K=4 on 17 and 24 pairs (ks_rows2 runs of 5-6 ciphertexts: the
-    cross-ciphertext prefetch, key-tile reuse and accumulator restart), 17
-    pairs in chunks of 5/5/5/2 (the multi-chunk loop, a short last chunk) and
-    the bench's own 256 pairs (two 128-pair chunks of the 8 GiB workspace,
-    runs of 8), every output residue compared with the oracle."""
+    dnum=2, K=4 on 17 and 24 pairs (the split key switch's pair ranges of
+    5-8 pairs per workgroup, two or three per quarter stream: the next pair's
+    prefetch, the key tile shared by the quarters and reused across pairs,
+    the accumulator restart), 17 pairs in chunks of 5/5/5/2 (the multi-chunk
+    loop, a short last chunk) and the bench's own 256 pairs (two 128-pair
+    chunks of the 8 GiB workspace, about 3 pairs per quarter), every output
+    residue compared with the oracle."""
     if chunk:
         monkeypatch.setenv("GPQHE_CHUNK", str(chunk))
     want, got = mul_batch_both(oracle, product, name, cnt, seeds=(21, 22))
