@@ -1044,13 +1044,15 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
     gpqhe_die("he_mul_rescale_batch: bad level %u", lvl);
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  const size_t per_ct = (size_t)(2 * lvl + 2 * lvl + ndig * nm + 2 * nm + 2 * lvl) * n * 8;
-  // workspace per chunk (GPQHE_WS_MIB, default 8 GiB: 170 pairs at N=2^16, L=8,
-  // dnum=2, so the bench's 256 pairs run as 2 chunks of 128).  Bigger chunks
-  // fill the GPU better (dn_cols has 32 blocks per pair) and amortize
-  // ks_rows2's key tiles over more runs: same-box A/B 27.3k (2 GiB) vs
-  // 28.3-28.6k (2.5-4 GiB); later 32.3-32.7k (4 GiB) vs 33.5k (8 GiB) vs
-  // 33.3k (16 GiB, one chunk).  288 GB of HBM leave room.
+  // workspace limbs per pair: the split key switch holds y, T1, the dropped
+  // slots and conv; the streaming one d2, y, T1 and both accumulators
+  const size_t per_ct = (k_mul_split_ok(lvl) ? (size_t)(lvl + ndig * nm + 2 * (G.K + 1) + 2 * lvl)
+                                              : (size_t)(2 * lvl + 2 * lvl + ndig * nm + 2 * nm + 2 * lvl)) * n * 8;
+  // workspace per chunk (GPQHE_WS_MIB, default 8 GiB: 292 pairs at N=2^16,
+  // L=8, dnum=2 on the split key switch, so the bench's 256 pairs run as one
+  // chunk: 39.7k vs 38.4k ct-mult/s for two chunks of 128, same box).  Bigger
+  // chunks fill the GPU better and amortize the key tiles over more pairs;
+  // 288 GB of HBM leave room.
   static const size_t budget = (size_t)env_u("GPQHE_WS_MIB", 8192) << 20;
   size_t chunk = std::max<size_t>(1, budget / per_ct);
   chunk = std::min<size_t>(chunk, 65535 / (ndig * nm));

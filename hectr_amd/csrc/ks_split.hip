@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
   // LTW: the tile's row-pass twiddles (RowTw), read by every quarter: with
   // every modulus on FP64 (ALLF) forward and inverse as 8-byte entries, else
   // the forward ones as 16-byte entries
-  constexpr int TWW = !LTW ? 2 : ALLF ? 2 * RowTw<LOGN2>::ENTRIES : 2 * RowTw<LOGN2>::ENTRIES;
+  constexpr int TWW = !LTW ? 2 : (ALLF && KEEP) ? RowTw<LOGN2>::ENTRIES : 2 * RowTw<LOGN2>::ENTRIES;
   __shared__ __attribute__((aligned(16))) uint64_t rtw[TWW];
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
@@ -96,8 +96,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
     constexpr bool W8 = LTW && ALLF;  // ALLF: A0 is ArF64
     if constexpr (W8) {
       RowTw<LOGN2>::template stage<true>(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
-      RowTw<LOGN2>::template stage<true>(rtw + RowTw<LOGN2>::ENTRIES, (const uint64_t *)ar0.itw, n1 + row0,
-                                         threadIdx.x, 256 * QN);
+      if constexpr (!KEEP)  // the dropped slots' inverse row pass
+        RowTw<LOGN2>::template stage<true>(rtw + RowTw<LOGN2>::ENTRIES, (const uint64_t *)ar0.itw, n1 + row0,
+                                           threadIdx.x, 256 * QN);
       __syncthreads();
     } else if constexpr (LTW) {
       RowTw<LOGN2>::stage(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     const auto ar = [&] {
       if constexpr (LTW)
         return row_policy<LOGN2, W8>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
-                                     W8 ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
+                                     W8 && !KEEP ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
       else
         return ar0;
     }();
@@ -296,9 +297,10 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
                        unsigned nm, unsigned t_lo, unsigned t_n)
 {
   const unsigned n = G.n, groups = t_n * (n / 2048);
-  // pair ranges of about 3 pairs per quarter; more, shorter ranges while the
-  // grid would not give every CU two workgroups
-  const unsigned per = 3 * QN;
+  // pair ranges of about 8 pairs per quarter stream (128 pairs at N=2^16:
+  // 3 pairs 38.5k, 5-50 pairs 39.2-39.3k ct-mult/s, same box); more, shorter
+  // ranges while the grid would not give every CU two workgroups
+  const unsigned per = 8 * QN;
   unsigned members = std::max(1u, (count + per - 1) / per);
   while (members < count && (size_t)groups * members < 2 * 256)
     members++;
@@ -324,6 +326,7 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
     ksq_launch<LOGN2, 1, 4, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
     break;
   case 2:
+    // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
     if (allf)
       ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
     else
