@@ -123,12 +123,39 @@ static void stage_release()
 }
 
 // ===========================================================================
-// Helpers
+// Deferred encode + public-key encryption (the small-N latency path).
+//
+// HECTR encodes and encrypts its five state vectors back to back every control
+// step (src/ctr.c:466-475), then frees the plaintexts.  Each he_ecd (host FFT,
+// upload, lift + NTT) and he_enc_pk (sample v, e0, e1, NTT, combine) is queued
+// instead of launched, and the queue runs as one batch -- one upload, one
+// lift + NTT, one sampling, one NTT and one combine launch for all of them --
+// when anything else touches the engine (every other entry point flushes
+// first).  The RNG streams are taken at call time, so the results are the
+// ones of the sequential calls bit for bit.
 // ===========================================================================
+struct PendEcd {
+  uint64_t *dst;
+  unsigned lvl;
+};
+struct PendEnc {
+  uint64_t *c0, *c1;
+  const uint64_t *m, *pk0, *pk1;
+  unsigned lvl;
+  uint64_t stream;
+};
+static std::vector<PendEcd> g_pecd;
+static std::vector<int64_t> g_pcoef;  // n coefficients per pending encode
+static std::vector<PendEnc> g_penc;
+
+static void flush_pending();
+
 static void check_ctx()
 {
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
+  if (!g_pecd.empty() || !g_penc.empty())
+    flush_pending();
 }
 
 static inline he_ct_t *OB(void *o) { return (he_ct_t *)o; }
@@ -189,6 +216,8 @@ static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
 
 static void obj_free(void *vo)
 {
+  if (G.init)
+    check_ctx();  // a queued encode / encryption may still use the payload
   he_ct_t *o = OB(vo);
   if (o->data && G.init)
     pool_free(o->data);
@@ -280,6 +309,8 @@ static void set_seed_words(uint64_t seed)
 
 extern "C" void gpqhe_set_seed(uint64_t seed)
 {
+  if (G.init)
+    check_ctx();  // queued encryptions sample with the current key
   set_seed_words(seed);
 }
 
@@ -395,6 +426,7 @@ extern "C" void hectx_exit(void)
 {
   if (!G.init)
     return;
+  check_ctx();
   HIP_CHECK(hipStreamSynchronize(G.stream));
   gemv_cache_clear();
   tables_free();
@@ -423,6 +455,8 @@ extern "C" void hectx_info(gpqhe_info_t *info)
 
 extern "C" void gpqhe_set_stream(void *stream)
 {
+  if (G.init)
+    check_ctx();
   if (G.stream)
     HIP_CHECK(hipStreamSynchronize(G.stream));
   G.stream = stream ? (hipStream_t)stream : G.own_stream;
@@ -430,6 +464,8 @@ extern "C" void gpqhe_set_stream(void *stream)
 
 extern "C" void gpqhe_sync(void)
 {
+  if (G.init)
+    check_ctx();
   if (G.stream)
     HIP_CHECK(hipStreamSynchronize(G.stream));
 }
@@ -606,6 +642,69 @@ static unsigned gpu_ecd_min()
   return m;
 }
 
+// Deferral applies to host-FFT encodes at n <= 2^12 (the whole-limb NTT
+// lifts in-kernel) into q limbs 0..lvl-1.
+static bool defer_ok(unsigned s)
+{
+  static const bool on = env_u("GPQHE_DEFER", 1) != 0;
+  return on && G.logn <= 12 && G.logn >= 10 && s < gpu_ecd_min();
+}
+
+static void flush_pending()
+{
+  std::vector<PendEcd> ecd;
+  std::vector<PendEnc> enc;
+  std::vector<int64_t> coef;
+  ecd.swap(g_pecd);
+  enc.swap(g_penc);
+  coef.swap(g_pcoef);
+  const size_t n = G.n;
+  if (!ecd.empty()) {
+    Ws dcoef(ecd.size() * n);
+    upload(dcoef.p, coef.data(), coef.size() * 8);
+    for (size_t i0 = 0; i0 < ecd.size();) {
+      // one launch per run of equal levels (at most GPQHE_MAXGRP polys)
+      size_t i1 = i0 + 1;
+      while (i1 < ecd.size() && i1 - i0 < GPQHE_MAXGRP && ecd[i1].lvl == ecd[i0].lvl)
+        i1++;
+      unsigned mods[GPQHE_MAXMOD];
+      for (unsigned l = 0; l < ecd[i0].lvl; l++)
+        mods[l] = l;
+      LimbSet ls = limbset(nullptr, mods, ecd[i0].lvl, (unsigned)(i1 - i0), 0);
+      ls.ngp = (uint32_t)(i1 - i0);
+      for (size_t i = i0; i < i1; i++)
+        ls.gp[i - i0] = ecd[i].dst;
+      k_lift_ntt(ls, (const int64_t *)dcoef.p + i0 * n);
+      i0 = i1;
+    }
+  }
+  for (size_t i0 = 0; i0 < enc.size();) {
+    // a run of encryptions at one level with consecutive RNG streams and the
+    // same public key
+    size_t i1 = i0 + 1;
+    while (i1 < enc.size() && i1 - i0 < GPQHE_MAXGRP && enc[i1].lvl == enc[i0].lvl &&
+           enc[i1].stream == enc[i0].stream + 3 * (i1 - i0) && enc[i1].pk0 == enc[i0].pk0)
+      i1++;
+    const unsigned k = (unsigned)(i1 - i0), lvl = enc[i0].lvl;
+    const size_t w = (size_t)lvl << G.logn;
+    unsigned mods[GPQHE_MAXMOD];
+    for (unsigned l = 0; l < lvl; l++)
+      mods[l] = l;
+    Ws vee(3 * k * w);
+    LimbSet s = limbset(vee.p, mods, lvl, 3 * k, w);
+    k_sample_enc(s, enc[i0].stream, 3 * k);
+    k_ntt(s, false);
+    EncBatch b{};
+    for (unsigned e = 0; e < k; e++) {
+      b.c0[e] = enc[i0 + e].c0;
+      b.c1[e] = enc[i0 + e].c1;
+      b.m[e] = enc[i0 + e].m;
+    }
+    k_enc_combine_batch(b, k, vee.p, enc[i0].pk0, enc[i0].pk1, lvl);
+    i0 = i1;
+  }
+}
+
 static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scale, const unsigned *mods,
                          unsigned nm)
 {
@@ -626,13 +725,32 @@ static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scal
 extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int slots, double scale,
                           unsigned int nlimbs)
 {
-  check_ctx();
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
+  if (!defer_ok(slots))
+    check_ctx();
   if (nlimbs < 1 || nlimbs > G.L)
     gpqhe_die("he_ecd_ex: bad level %u", nlimbs);
-  unsigned mods[GPQHE_MAXMOD];
-  for (unsigned i = 0; i < nlimbs; i++)
-    mods[i] = i;
-  encode_limbs(pt->data, (const double *)z, slots, scale, mods, nlimbs);
+  if (defer_ok(slots)) {
+    // queued (flush_pending); a plaintext a queued encryption still reads, or
+    // a queued encode target, is flushed first
+    bool busy = false;
+    for (const PendEnc &e : g_penc)
+      busy |= e.m == pt->data || e.c0 == pt->data;
+    for (const PendEcd &e : g_pecd)
+      busy |= e.dst == pt->data;
+    if (busy)
+      flush_pending();
+    const size_t at = g_pcoef.size();
+    g_pcoef.resize(at + G.n);
+    hm_encode_coeffs(g_pcoef.data() + at, (const double *)z, slots, G.n, scale);
+    g_pecd.push_back({pt->data, nlimbs});
+  } else {
+    unsigned mods[GPQHE_MAXMOD];
+    for (unsigned i = 0; i < nlimbs; i++)
+      mods[i] = i;
+    encode_limbs(pt->data, (const double *)z, slots, scale, mods, nlimbs);
+  }
   pt->nlimbs = nlimbs;
   pt->scale = scale;
   pt->flags = 0;
@@ -665,8 +783,28 @@ extern "C" void he_dcd(gpqhe_complex_t z[], const he_pt_t *pt)
 
 extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
 {
-  check_ctx();
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
   const unsigned lvl = pt->nlimbs;
+  if (defer_ok(0)) {
+    // queued (flush_pending): streams taken now, in call order
+    bool busy = false;
+    for (const PendEnc &e : g_penc)
+      busy |= e.m == ct->data || e.c0 == ct->data;
+    for (const PendEcd &e : g_pecd)
+      busy |= e.dst == ct->data;
+    if (busy)
+      flush_pending();
+    const uint64_t stream = next_stream();
+    next_stream();
+    next_stream();
+    g_penc.push_back({limb(ct, 0, 0), limb(ct, 1, 0), pt->data, limb(pk, 0, 0), limb(pk, 1, 0), lvl, stream});
+    ct->nlimbs = lvl;
+    ct->scale = pt->scale;
+    ct->flags = 0;
+    return;
+  }
+  check_ctx();
   const size_t w = (size_t)lvl << G.logn;
   unsigned mods[GPQHE_MAXMOD];
   for (unsigned i = 0; i < lvl; i++)

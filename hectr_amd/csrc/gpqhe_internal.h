@@ -168,15 +168,22 @@ __host__ __device__ __forceinline__ uint64_t splitmix64_mix(uint64_t z)
 // Limb sets: `count` limbs, limb v at base + (v / per) * stride + (v % per) * n,
 // reduced modulo mods[v % per].  Passed by value to kernels.
 // ---------------------------------------------------------------------------
+#define GPQHE_MAXGRP 8
 struct LimbSet {
   uint64_t *base;
   size_t stride;      // words between groups of `per` limbs
   uint32_t per;
   uint32_t count;
   uint8_t mods[GPQHE_MAXMOD];
+  // ngp > 0: group g starts at gp[g] instead (separately allocated objects
+  // batched into one launch, g < ngp <= GPQHE_MAXGRP)
+  uint64_t *gp[GPQHE_MAXGRP];
+  uint32_t ngp;
 
   __host__ __device__ __forceinline__ uint64_t *limb(uint32_t v, uint32_t logn) const
   {
+    if (ngp)
+      return gp[v / per] + ((size_t)(v % per) << logn);
     return base + (size_t)(v / per) * stride + ((size_t)(v % per) << logn);
   }
   __host__ __device__ __forceinline__ uint32_t mod(uint32_t v) const { return mods[v % per]; }
@@ -251,9 +258,17 @@ void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);
 void k_lift_i64(const LimbSet &dst, const int64_t *coef);
-void k_lift_ntt(const LimbSet &dst, const int64_t *coef);  // lift + forward NTT
+void k_lift_ntt(const LimbSet &dst, const int64_t *coef);  // lift + forward NTT (group g: coef + g n)
 void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
                    const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl);
+// up to GPQHE_MAXGRP public-key encryptions in one launch: encryption i takes
+// v, e0, e1 from vee + (3 i + {0, 1, 2}) * lvl * n
+struct EncBatch {
+  uint64_t *c0[GPQHE_MAXGRP], *c1[GPQHE_MAXGRP];
+  const uint64_t *m[GPQHE_MAXGRP];
+};
+void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, const uint64_t *pk0,
+                         const uint64_t *pk1, unsigned lvl);
 void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,
                       unsigned lvl);
 void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *sprime,

@@ -460,7 +460,8 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
 #pragma unroll
         for (int k = 0; k < 8; k++)
           a[k] = r ? A::unbits(lds[pos0 + k * d8])
-                   : A::load(coef ? lift_i64(coef[pos0 + k * d8], mc) : x[pos0 + k * d8]);
+                   : A::load(coef ? lift_i64(coef[((size_t)(v / s.per) << LOGN) + pos0 + k * d8], mc)
+                                  : x[pos0 + k * d8]);
         ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
         if (r + 1 < FULL || REM) {
 #pragma unroll
@@ -827,7 +828,7 @@ __global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uin
   uint32_t b[16];
   chacha20_block(b, key, stream + y, k);
   int v;
-  if (y) {
+  if (y % 3) {  // (v, e0, e1) per encryption: ternary v, CBD e0 / e1
     v = __popc(b[0] & 0x1FFFFFu) - __popc(b[1] & 0x1FFFFFu);
   } else {
     const uint32_t r = b[0] & 3u;
@@ -1045,6 +1046,29 @@ void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t
 {
   hipLaunchKernelGGL(enc_kernel, dim3((G.n + TPB - 1) / TPB, lvl), dim3(TPB), 0, G.stream, c0, c1, v, e0, e1, pk0,
                      pk1, m, G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
+__global__ void enc_batch_kernel(EncBatch bt, const uint64_t *vee, const uint64_t *pk0, const uint64_t *pk1,
+                                 unsigned logn, unsigned lvl, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const unsigned e = blockIdx.z;
+  const ModConst m = mc[blockIdx.y];
+  const size_t o = ((size_t)blockIdx.y << logn) + i, w = (size_t)lvl << logn;
+  const uint64_t *v = vee + 3 * e * w;
+  bt.c0[e][o] = add_mod(add_mod(v[w + o], mul_mod(v[o], pk0[o], m), m.q), bt.m[e][o], m.q);
+  bt.c1[e][o] = add_mod(v[2 * w + o], mul_mod(v[o], pk1[o], m), m.q);
+}
+
+void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, const uint64_t *pk0,
+                         const uint64_t *pk1, unsigned lvl)
+{
+  hipLaunchKernelGGL(enc_batch_kernel, dim3((G.n + TPB - 1) / TPB, lvl, k), dim3(TPB), 0, G.stream, b, vee, pk0, pk1,
+                     G.logn, lvl, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -22,4 +22,4 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     env "${v#*=}" timeout -k 10 300 $B > $OUT/bench_${v%%=*}_$r.log 2>&1 || exit 1
   done
 done
-python scripts/ab_summary.py ${RUN:-libab} || true
+python scripts/ab_summary.py $OUT || true
