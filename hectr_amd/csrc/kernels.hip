@@ -1553,9 +1553,12 @@ __global__ void __launch_bounds__(256) ks_cols_kernel(const uint64_t *ybuf, size
     for (int k = 0; k < 16; k++)
       r[k] = lds[(16 * g + k) * CP + c];
     fwd_stages<4>(r, tw2, T + 16 * g, 3, q);
+    const bool f64 = q < F64_QMAX && tw.fwdd;  // T1 is read lazily: doubles on FP64 moduli
 #pragma unroll
-    for (int k = 0; k < 16; k++)
-      out[(size_t)(16 * g + k) * n2 + c] = canon4(r[k], q, q2);
+    for (int k = 0; k < 16; k++) {
+      const uint64_t v = canon4(r[k], q, q2);
+      out[(size_t)(16 * g + k) * n2 + c] = f64 ? (uint64_t)__double_as_longlong((double)v) : v;
+    }
   }
 }
 
@@ -1718,7 +1721,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        (out + (size_t)k * n2)[vo] = ar.canon(r[k]);
+        (out + (size_t)k * n2)[vo] = ar.store_lazy(r[k]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }
@@ -1819,7 +1822,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
         const uint64_t *x = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
 #pragma unroll
         for (int k = 0; k < 8; k++)
-          r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+          r[k] = A::load_lazy(x[(row << LOGN2) + l + T::TA * k]);
         __syncthreads();
         rows8_fwd_raw<LOGN2>(r, lds, ar, n1 + row0);
       }
@@ -2432,7 +2435,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        (out + (size_t)k * n2)[vo] = ar.canon(r[k]);
+        (out + (size_t)k * n2)[vo] = ar.store_lazy(r[k]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }
@@ -2474,7 +2477,7 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
     typename A::V r[8];
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+      r[k] = A::load_lazy(x[(row << LOGN2) + l + T::TA * k]);  // conv (dn_cols, lazy)
     rows8_fwd<LOGN2>(r, cv, lds, ar, n1 + row0);
   });
   wave_sync();

@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
         V r[8];
 #pragma unroll
         for (int k = 0; k < 8; k++)
-          r[k] = A::load(xn[u][k]);
+          r[k] = A::load_lazy(xn[u][k]);  // T1 (ks_cols4, lazy)
         if (pn < pb1)
           fetch(xn[u], j, pn);  // next pair's tile, in flight meanwhile
         wave_sync();            // the previous phase has finished with the LDS tile
@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            r[k] = A::load(cv[(row << LOGN2) + l + T::TA * k]);
+            r[k] = A::load_lazy(cv[(row << LOGN2) + l + T::TA * k]);  // conv (dn_cols, lazy)
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           uint64_t o[8];

@@ -176,6 +176,10 @@ struct ArInt {
   const uint64_t *itw;  // and inverse
   __device__ static V load(uint64_t x) { return x; }
   __device__ uint64_t canon(V x) const { return canon4(x, q, 2 * q); }  // x < 4q
+  // forward-transform intermediates between a column and a row pass (T1,
+  // conv, the NTT's own): canonical words on integer moduli
+  __device__ static V load_lazy(uint64_t b) { return b; }
+  __device__ uint64_t store_lazy(V x) const { return canon(x); }
   __device__ static uint64_t bits(V x) { return x; }
   __device__ static V unbits(uint64_t b) { return b; }
   template <int LE>
@@ -194,6 +198,11 @@ struct ArF64 {
   const double *itw;  // and inverse
   __device__ static V load(uint64_t x) { return f64_from_u52(x); }  // x canonical (< q)
   __device__ uint64_t canon(V x) const { return f64_canon(x, q, qinv); }
+  // forward-transform intermediates (T1, conv, the NTT's own): the lazy
+  // double itself (|x| < 2q, an exact integer), no canonicalisation, no
+  // conversion -- a stage boundary inside one pass sees the same values
+  __device__ static V load_lazy(uint64_t b) { return unbits(b); }
+  __device__ static uint64_t store_lazy(V x) { return bits(x); }
   __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
   __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
   template <int LE>
@@ -465,7 +474,7 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
     ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
     for (int k = 0; k < 16; k++)
-      (y + (size_t)k * n2)[vo] = ar.canon(r[k]);
+      (y + (size_t)k * n2)[vo] = ar.store_lazy(r[k]);  // the row pass (ntt3_rows) reads it lazily
   } else {
     {
       const int c = t % C, g = t / C;
@@ -729,7 +738,7 @@ __device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint6
     const int l = th % T::TA;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      r[k] = A::load(x[(row << LOGN2) + l + T::TA * k]);
+      r[k] = A::load_lazy(x[(row << LOGN2) + l + T::TA * k]);  // written by cols_tile<fwd>
     uint64_t out[8];
     rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0);
     const int h = th % T::TA;
