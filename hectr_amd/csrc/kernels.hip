@@ -1991,18 +1991,48 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   const unsigned row0 = tile * T::R;
   const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
   const uint64_t *pa = a + p * in_stride + in_pstride + off, *pb = b + p * in_stride + in_pstride + off;
-  uint64_t raw[8];
+  // this thread's 8 consecutive words 8 th + k are exactly its round-C
+  // elements of the inverse row pass: 16-byte loads, no transpose through LDS
+  const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
+  uint64_t A1[8], B1[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-    raw[i] = mulmod_vv(pa[wl_elem(i)], pb[wl_elem(i)], mc);
-  if (d2) {  // the NTT-form copy for the streaming ks_rows (the split key switch forms it from a, b)
-    uint64_t *dn = d2 + (size_t)p * lvl * ((size_t)1 << logn) + off;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-      dn[wl_elem(i)] = raw[i];
+  for (int i = 0; i < 4; i++) {
+    const ulonglong2 x = ((const ulonglong2 *)(pa + 8 * th))[i], z = ((const ulonglong2 *)(pb + 8 * th))[i];
+    A1[2 * i] = x.x;
+    A1[2 * i + 1] = x.y;
+    B1[2 * i] = z.x;
+    B1[2 * i + 1] = z.y;
   }
   uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
-  with_arith(mc.q, limb, logn, tw, [&](const auto &ar) { rows8_tile_raw<LOGN2, true>(ar, raw, yo, lds, n1 + row0); });
+  with_arith(mc.q, limb, logn, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    typename A::V r[8];
+    uint64_t raw[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if constexpr (std::is_same<A, ArF64>::value) {
+        // exact FP64 product of canonical residues, |.| < 1.5 q (a valid
+        // inverse-pass input); canonical only for the optional d2 copy
+        const double bb = f64_from_u52(B1[k]);
+        r[k] = f64_mulmod(f64_from_u52(A1[k]), bb, bb * ar.qinv, ar.q);
+        if (d2)
+          raw[k] = ar.canon(r[k]);
+      } else {
+        raw[k] = mul_mod(A1[k], B1[k], mc);
+        r[k] = A::load(raw[k]);
+      }
+    }
+    if (d2) {  // the NTT-form copy for the streaming ks_rows (the split key switch forms it from a, b)
+      ulonglong2 *dn = (ulonglong2 *)(d2 + (size_t)p * lvl * ((size_t)1 << logn) + off + 8 * th);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        dn[i] = make_ulonglong2(raw[2 * i], raw[2 * i + 1]);
+    }
+    rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      yo[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+  });
 }
 
 bool k_ks_fused_ok()
