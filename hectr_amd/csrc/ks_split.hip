@@ -124,6 +124,39 @@ __global__ void __launch_bounds__(256 * QN, 1)
           f0[k] = f1[k] = 0;
           a0[k] = a1[k] = 0;
         }
+      // the dropped q slot's first half of input words is requested here, so
+      // its latency overlaps the converted limb's row pass (1037 -> 1018 us)
+      const size_t ioff = p * d01.in_stride + ((size_t)t << logn) + toff + 8 * th;
+      const uint64_t *pin[4] = {d01.a + ioff, d01.b + ioff, d01.a + ioff + d01.in_pstride,
+                                d01.b + ioff + d01.in_pstride};  // a0, b0, a1, b1
+      uint64_t inw[4][4];
+      auto ld_in = [&](int h) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+          const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4 * h);
+          const ulonglong2 w0 = v2[0], w1 = v2[1];
+          inw[a][0] = w0.x;
+          inw[a][1] = w0.y;
+          inw[a][2] = w1.x;
+          inw[a][3] = w1.y;
+        }
+      };
+      // (the kept slots' kernel cannot hold them: requesting the conv and
+      // input words here spilled at three streams, 1.89 -> 2.73 ms per chunk,
+      // and two streams with the room for them ran 2.04 vs 1.90 ms)
+      constexpr bool EARLY = !KEEP;
+      uint64_t cvw[KEEP && EARLY ? 2 : 1][8];
+      if constexpr (KEEP && EARLY) {
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+          const uint64_t *cv = conv + (((size_t)(2 * p + half) * t_n + t) << logn) + toff;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            cvw[half][k] = cv[(row << LOGN2) + l + T::TA * k];
+        }
+      }
+      if (EARLY && jo < NDIG)
+        ld_in(0);
 #pragma unroll
       for (int u = 0; u < NX; u++) {
         if (u >= nx)
@@ -165,34 +198,22 @@ __global__ void __launch_bounds__(256 * QN, 1)
       if (jo < NDIG) {
         // q limb: own digit x = a1 b1 (the NTT-form d2 limb) and P (d0, d1),
         // from the four input words at this thread's natural positions 8 th + k
-        const size_t off = p * d01.in_stride + ((size_t)t << logn) + toff + 8 * th;
-        const uint64_t *pa = d01.a + off, *pb = d01.b + off;
         if constexpr (F) {
           const double Pd = f64_from_u52(mc.pmod), Pq = Pd * ar.qinv;
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            double A0[4], A1[4], B0[4], B1[4];
-            auto ld4 = [&](const uint64_t *s, double (&x)[4]) {
-              const ulonglong2 *v2 = (const ulonglong2 *)(s + 4 * h);
-              const ulonglong2 w0 = v2[0], w1 = v2[1];
-              x[0] = f64_from_u52(w0.x);
-              x[1] = f64_from_u52(w0.y);
-              x[2] = f64_from_u52(w1.x);
-              x[3] = f64_from_u52(w1.y);
-            };
-            ld4(pa, A0);
-            ld4(pb, B0);
-            ld4(pa + d01.in_pstride, A1);
-            ld4(pb + d01.in_pstride, B1);
+            if (h || !EARLY)
+              ld_in(h);
 #pragma unroll
             for (int e = 0; e < 4; e++) {
               const int k = 4 * h + e;
+              const double A0 = f64_from_u52(inw[0][e]), B0 = f64_from_u52(inw[1][e]);
+              const double A1 = f64_from_u52(inw[2][e]), B1 = f64_from_u52(inw[3][e]);
               const double eb = __longlong_as_double((long long)kl[2 * jo][256 * k + th]);
               const double ea = __longlong_as_double((long long)kl[2 * jo + 1][256 * k + th]);
-              const double x = f64_mulmod(A1[e], B1[e], B1[e] * ar.qinv, ar.q);  // |x| < 1.5 q
-              const double d0 = f64_mulmod(A0[e], B0[e], B0[e] * ar.qinv, ar.q);
-              const double d1 = f64_red(f64_mulmod(A0[e], B1[e], B1[e] * ar.qinv, ar.q) +
-                                            f64_mulmod(A1[e], B0[e], B0[e] * ar.qinv, ar.q),
+              const double x = f64_mulmod(A1, B1, B1 * ar.qinv, ar.q);  // |x| < 1.5 q
+              const double d0 = f64_mulmod(A0, B0, B0 * ar.qinv, ar.q);
+              const double d1 = f64_red(f64_mulmod(A0, B1, B1 * ar.qinv, ar.q) + f64_mulmod(A1, B0, B0 * ar.qinv, ar.q),
                                         ar.q, ar.qinv);
               // |f| <= q/2 + 1.5 q after the fold, then + two products < 1.5 q
               const double g0 = f64_red(f0[k], ar.q, ar.qinv) + f64_mulmod(x, eb, eb * ar.qinv, ar.q);
@@ -204,26 +225,17 @@ __global__ void __launch_bounds__(256 * QN, 1)
         } else {
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            uint64_t A0[4], A1[4], B0[4], B1[4];
-            auto ld4 = [&](const uint64_t *s, uint64_t (&x)[4]) {
-              const ulonglong2 *v2 = (const ulonglong2 *)(s + 4 * h);
-              const ulonglong2 w0 = v2[0], w1 = v2[1];
-              x[0] = w0.x;
-              x[1] = w0.y;
-              x[2] = w1.x;
-              x[3] = w1.y;
-            };
-            ld4(pa, A0);
-            ld4(pb, B0);
-            ld4(pa + d01.in_pstride, A1);
-            ld4(pb + d01.in_pstride, B1);
+            if (h || !EARLY)
+              ld_in(h);
 #pragma unroll
             for (int e = 0; e < 4; e++) {
               const int k = 4 * h + e;
-              mac_i(a0[k], mul_mod(A1[e], B1[e], mc), kl[2 * jo][256 * k + th]);
-              mac_i(a1[k], mul_mod(A1[e], B1[e], mc), kl[2 * jo + 1][256 * k + th]);
-              const uint64_t d0 = mul_mod(A0[e], B0[e], mc);
-              const uint64_t d1 = add_mod(mul_mod(A0[e], B1[e], mc), mul_mod(A1[e], B0[e], mc), q);
+              const uint64_t A0 = inw[0][e], B0 = inw[1][e], A1 = inw[2][e], B1 = inw[3][e];
+              const uint64_t x = mul_mod(A1, B1, mc);
+              mac_i(a0[k], x, kl[2 * jo][256 * k + th]);
+              mac_i(a1[k], x, kl[2 * jo + 1][256 * k + th]);
+              const uint64_t d0 = mul_mod(A0, B0, mc);
+              const uint64_t d1 = add_mod(mul_mod(A0, B1, mc), mul_mod(A1, B0, mc), q);
               const uint64_t c0 = a0[k] >= q ? a0[k] - q : a0[k], c1 = a1[k] >= q ? a1[k] - q : a1[k];
               a0[k] = add_mod(c0, mul_shoup(d0, mc.pmod, mc.pmodp, q), q);
               a1[k] = add_mod(c1, mul_shoup(d1, mc.pmod, mc.pmodp, q), q);
@@ -247,7 +259,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            r[k] = A::load_lazy(cv[(row << LOGN2) + l + T::TA * k]);  // conv (dn_cols, lazy)
+            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           uint64_t o[8];
