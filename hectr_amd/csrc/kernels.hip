@@ -2665,7 +2665,10 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
   case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
   case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
   case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
-  case 16: mul_split_launch<8, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  // 2^16 = 128 x 512: one NTT stage moves from the VALU-bound column kernels
+  // to the row passes of the memory-bound ksq kernels (41.5-41.9k -> 42.0k
+  // ct-mult/s against 256 x 256, same box)
+  case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
   case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
   default: gpqhe_die("split key switch needs 2^13 <= n <= 2^17");
   }
