@@ -247,6 +247,13 @@ def roofline(stats, total_s, mb, workload, pairs_per_launch):
         for k in ("valu_busy", "sq_wait_any", "mean_us"):
             if k in e:
                 dom["pmc_" + k] = e[k]
+        # what limits the kernel: its measured HBM rate against the peak beside
+        # its VALU busy fraction (integer/FP64 work, no MFMA on this path)
+        hbm_frac = e["hbm_bytes"] / e["mean_us"] / 1e3 / HBM_PEAK_GBS
+        dom["pmc_hbm_frac"] = hbm_frac
+        if "valu_busy" in e:
+            dom["limiter"] = "valu" if e["valu_busy"] > hbm_frac else "hbm"
+            dom["bound"] = dom["limiter"]
     if prof:
         pipe = [pmc_entry(prof, k) for k in PIPELINE]
         if all(pipe):

@@ -318,8 +318,12 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d2, uint64_t *ybuf, uint64
 // conversion, then the kept slots' inner product with the ModDown epilogue).
 // out may equal a or b only with one pair and out_pstride == in_pstride.
 bool k_mul_split_ok(unsigned lvl);
+// ws: a workspace of k_mul_split_ws_words(count, lvl, rescale) words, or null
+// (the pool's, on the engine stream)
+size_t k_mul_split_ws_words(unsigned count, unsigned lvl, bool rescale);
 void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
-                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale);
+                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale,
+                       uint64_t *ws = nullptr);
 // ModDown (mode 0: / P, 1: / P q_{lvl-1}) of X whose drop limbs hold the
 // inverse row pass of their NTT form (k_mul_keyswitch_fused with drop_lo =
 // keep).

@@ -2620,7 +2620,7 @@ bool k_mul_split_ok(unsigned lvl)
 template <int LOGT1, int LOGN2>
 static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
                              size_t in_stride, size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl,
-                             bool rescale)
+                             bool rescale, uint64_t *ws)
 {
   const UpTable &up = up_table(lvl);
   const DownTable &dn = down_table(lvl, rescale ? 1 : 0);
@@ -2629,10 +2629,14 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
     gpqhe_die("split key switch: ModDown over %u moduli unsupported (max 5)", nd);
   const unsigned na_min = lvl - (ndig - 1) * G.alpha;
   const bool invc = G.alpha <= 4 && nm - na_min <= 8;
-  uint64_t *y = (uint64_t *)pool_alloc((size_t)count * lvl * n * 8);
-  uint64_t *T1 = (uint64_t *)pool_alloc((size_t)count * ndig * nm * n * 8);
-  uint64_t *accd = (uint64_t *)pool_alloc((size_t)2 * count * nd * n * 8);
-  uint64_t *conv = (uint64_t *)pool_alloc((size_t)2 * count * keep * n * 8);
+  // workspace: the caller's (k_mul_split_ws_words) or the pool's
+  const bool own = !ws;
+  if (own)
+    ws = (uint64_t *)pool_alloc(k_mul_split_ws_words(count, lvl, rescale) * 8);
+  uint64_t *y = ws;
+  uint64_t *T1 = y + (size_t)count * lvl * n;
+  uint64_t *accd = T1 + (size_t)count * ndig * nm * n;
+  uint64_t *conv = accd + (size_t)2 * count * nd * n;
   const D01Src d01{a, b, in_stride, in_pstride};
   const bool allf = up.f64 && dn.f64;
   d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc);
@@ -2652,24 +2656,29 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
     ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.dinv, dn.dinvp, count, lvl, nm, 0,
             keep);
   }
-  pool_free(conv);
-  pool_free(accd);
-  pool_free(T1);
-  pool_free(y);
+  if (own)
+    pool_free(ws);
+}
+
+size_t k_mul_split_ws_words(unsigned count, unsigned lvl, bool rescale)
+{
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
+  const unsigned nd = G.K + (rescale ? 1 : 0), keep = rescale ? lvl - 1 : lvl;
+  return (size_t)count * ((size_t)lvl + (size_t)ndig * nm + 2 * nd + 2 * keep) * G.n;
 }
 
 void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
-                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale)
+                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale, uint64_t *ws)
 {
   switch (G.logn) {
-  case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
-  case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
-  case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
+  case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
+  case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
   // 2^16 = 128 x 512: one NTT stage moves from the VALU-bound column kernels
   // to the row passes of the memory-bound ksq kernels (41.5-41.9k -> 42.0k
   // ct-mult/s against 256 x 256, same box)
-  case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
-  case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale); break;
+  case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
+  case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
   default: gpqhe_die("split key switch needs 2^13 <= n <= 2^17");
   }
 }

@@ -124,21 +124,34 @@ __device__ __forceinline__ uint64_t f64_canon(double x, double q, double qinv)
   return (uint64_t)__double_as_longlong(v + b) & ((1ull << 52) - 1);
 }
 
+// lz (moduli below 2^50): the reduction of the CT input X (forward) / of
+// U + V (inverse) is skipped on every odd stage of a call, so no two
+// consecutive stages skip it.  With |y| 2^-52 <= b/4 for |y| = b q, q < 2^50,
+// the quotient estimate is off by < 1/2 + b/4 and |T| <= q (1/2 + b/4): the
+// forward values stay below 2.55 q and the inverse ones below 3 q (fixed
+// points of the two-stage recurrences), every intermediate an exact integer
+// below 2^52 -- and canonical outputs bit-identical.
 template <int LE>
 __device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
-                                             int log_thi, double q, double qinv)
+                                             int log_thi, double q, double qinv, bool lz = false)
 {
   constexpr int E = 1 << LE;
 #pragma unroll
   for (int s = 0; s < LE; s++) {
     const uint64_t Bs = bb >> (log_thi - s + 1);
     const int half = E >> (s + 1);
+    if (!(lz && (s & 1))) {
+#pragma unroll
+      for (int k = 0; k < E; k++)
+        if (!(k & half))
+          x[k] = f64_red(x[k], q, qinv);
+    }
 #pragma unroll
     for (int k = 0; k < E; k++) {
       if (k & half)
         continue;
       const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
-      const double X = f64_red(x[k], q, qinv);
+      const double X = x[k];
       const double T = f64_mulmod(x[k + half], twd[i2], twd[i2 + 1], q);
       x[k] = X + T;
       x[k + half] = X - T;
@@ -148,21 +161,28 @@ __device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double 
 
 template <int LE>
 __device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
-                                             int log_tlo, double q, double qinv)
+                                             int log_tlo, double q, double qinv, bool lz = false)
 {
   constexpr int E = 1 << LE;
 #pragma unroll
   for (int s = 0; s < LE; s++) {
     const uint64_t Bs = bb >> (log_tlo + s + 1);
     const int half = 1 << s;
+    const bool red = !(lz && (s & 1));
 #pragma unroll
     for (int k = 0; k < E; k++) {
       if (k & half)
         continue;
       const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (s + 1)));
       const double U = x[k], V = x[k + half];
-      x[k] = f64_red(U + V, q, qinv);
+      x[k] = U + V;
       x[k + half] = f64_mulmod(U - V, twd[i2], twd[i2 + 1], q);
+    }
+    if (red) {
+#pragma unroll
+      for (int k = 0; k < E; k++)
+        if (!(k & half))
+          x[k] = f64_red(x[k], q, qinv);
     }
   }
 }
@@ -196,6 +216,7 @@ struct ArF64 {
   double q, qinv;
   const double *tw;   // this modulus' forward (w, w / q) pairs
   const double *itw;  // and inverse
+  bool lz = false;    // q < 2^50: lazy reduction on alternate stages (fwd_stages_f)
   __device__ static V load(uint64_t x) { return f64_from_u52(x); }  // x canonical (< q)
   __device__ uint64_t canon(V x) const { return f64_canon(x, q, qinv); }
   // forward-transform intermediates (T1, conv, the NTT's own): the lazy
@@ -208,12 +229,12 @@ struct ArF64 {
   template <int LE>
   __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
   {
-    fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv);
+    fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv, lz);
   }
   template <int LE>
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
-    inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv);
+    inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv, lz);
   }
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
   {
@@ -240,6 +261,7 @@ __device__ __forceinline__ double fbc_term(double y, double c, double cq, double
 }
 
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
+constexpr uint64_t F64_LAZY = 1ull << 50;  // and its lazy stage reduction below this
 
 // Forward row passes with the twiddles of one row tile staged in LDS.  A
 // 2^LOGN2-point row pass of global row rho uses, at its stage of level lam
@@ -300,12 +322,18 @@ struct ArF64Row : ArF64 {
       const int shift = log_thi - s + 1;
       const uint64_t Bs = bb >> shift;
       const int half = E >> (s + 1);
+      if (!(lz && (s & 1))) {  // lazy reduction: see fwd_stages_f
+#pragma unroll
+        for (int k = 0; k < E; k++)
+          if (!(k & half))
+            x[k] = f64_red(x[k], q, qinv);
+      }
 #pragma unroll
       for (int k = 0; k < E; k++) {
         if (k & half)
           continue;
         const double2 w = twf(rt.lds, rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift));
-        const double X = f64_red(x[k], q, qinv);
+        const double X = x[k];
         const double T = f64_mulmod(x[k + half], w.x, w.y, q);
         x[k] = X + T;
         x[k + half] = X - T;
@@ -330,8 +358,14 @@ struct ArF64Row : ArF64 {
             continue;
           const double2 w = twf(itl, rt.idx(Bs + (uint64_t)(k >> (s + 1)), shift));
           const double U = x[k], V_ = x[k + half];
-          x[k] = f64_red(U + V_, q, qinv);
+          x[k] = U + V_;
           x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
+        }
+        if (!(lz && (s & 1))) {  // lazy reduction: see inv_stages_f
+#pragma unroll
+          for (int k = 0; k < E; k++)
+            if (!(k & half))
+              x[k] = f64_red(x[k], q, qinv);
         }
       }
     }
@@ -394,7 +428,7 @@ __device__ __forceinline__ void with_arith(uint64_t q, unsigned m, unsigned logn
 {
   const size_t o = (size_t)m << (logn + 1);
   if (q < F64_QMAX && tw.fwdd)
-    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o, q < F64_LAZY});
   else
     f(ArInt{q, tw.fwd + o, tw.inv + o});
 }
@@ -413,7 +447,7 @@ __device__ __forceinline__ void with_arith_t(uint64_t q, unsigned m, unsigned lo
 {
   if constexpr (ALL_F64) {
     const size_t o = (size_t)m << (logn + 1);
-    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o});
+    f(ArF64{(double)q, 1.0 / (double)q, tw.fwdd + o, tw.invd + o, q < F64_LAZY});
   } else {
     with_arith(q, m, logn, tw, f);
   }
