@@ -124,13 +124,17 @@ __device__ __forceinline__ uint64_t f64_canon(double x, double q, double qinv)
   return (uint64_t)__double_as_longlong(v + b) & ((1ull << 52) - 1);
 }
 
-// lz (moduli below 2^50): the reduction of the CT input X (forward) / of
-// U + V (inverse) is skipped on every odd stage of a call, so no two
-// consecutive stages skip it.  With |y| 2^-52 <= b/4 for |y| = b q, q < 2^50,
-// the quotient estimate is off by < 1/2 + b/4 and |T| <= q (1/2 + b/4): the
-// forward values stay below 2.55 q and the inverse ones below 3 q (fixed
-// points of the two-stage recurrences), every intermediate an exact integer
-// below 2^52 -- and canonical outputs bit-identical.
+// Bounds (|y| = b q; the quotient estimate is off by < 1/2 + |y| 2^-52, so
+// |T| <= q (1/2 + |y| 2^-52), and every value must stay an exact integer
+// below 2^53):
+// * lz (q < 2^50): the reduction of the CT input X (forward) / of U + V
+//   (inverse) is skipped on every odd stage of a call.  Forward: b stays
+//   below 2.55.  Inverse: a 3-stage call maps b to 1 + b/2, a 4-stage call to
+//   2 + b; the chains between canonical values here are at most 4 + 4 stages,
+//   so b <= 5 (5 q < 2^52.4).
+// * q >= 2^50: X / U + V reduced every stage; the inverse products T grow by
+//   up to q/2 a stage, so they are reduced at the last stage of every call
+//   (<= 4 stages: b < 2.5).  Canonical outputs are bit-identical either way.
 template <int LE>
 __device__ __forceinline__ void fwd_stages_f(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
                                              int log_thi, double q, double qinv, bool lz = false)
@@ -182,6 +186,15 @@ __device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double 
 #pragma unroll
       for (int k = 0; k < E; k++)
         if (!(k & half))
+          x[k] = f64_red(x[k], q, qinv);
+    }
+    if (!lz && s == LE - 1) {
+      // q >= 2^50: |T| <= q/2 + |U - V| q 2^-52 can grow by q/2 a stage, so
+      // the products are reduced at the last stage of every call (calls span
+      // at most 4 stages: |.| < 2.5 q, exact, throughout)
+#pragma unroll
+      for (int k = 0; k < E; k++)
+        if (k & half)
           x[k] = f64_red(x[k], q, qinv);
     }
   }
@@ -297,9 +310,12 @@ struct RowTw {
 };
 
 // ArF64 / ArInt with the forward twiddles from a RowTw table (the inverse
-// stays on the global table).  ArF64Row<.., true>: 8-byte entries (w only;
-// w / q recomputed as w fl(1/q), which moves the quotient estimate by at most
-// one and so never a canonical result) for both directions (itl: inverse).
+// stays on the global table).  ArF64Row<.., true>: 8-byte entries (w only,
+// w / q recomputed as w fl(1/q)) for both directions (itl: inverse).  The
+// recomputed quotient constant widens the estimate's error to 1.5 |y| 2^-52,
+// so on moduli >= 2^50 the products are reduced every stage (inverse) and
+// every other stage (forward): |.| < 1.75 q throughout, exact; below 2^50
+// the lazy bounds of fwd_stages_f / inv_stages_f hold with room to spare.
 template <int LOGN2, bool W8 = false>
 struct ArF64Row : ArF64 {
   RowTw<LOGN2> rt;
@@ -334,7 +350,9 @@ struct ArF64Row : ArF64 {
           continue;
         const double2 w = twf(rt.lds, rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift));
         const double X = x[k];
-        const double T = f64_mulmod(x[k + half], w.x, w.y, q);
+        double T = f64_mulmod(x[k + half], w.x, w.y, q);
+        if (W8 && !lz && (s & 1))
+          T = f64_red(T, q, qinv);  // recomputed w/q on a wide modulus: see below
         x[k] = X + T;
         x[k + half] = X - T;
       }
@@ -360,11 +378,19 @@ struct ArF64Row : ArF64 {
           const double U = x[k], V_ = x[k + half];
           x[k] = U + V_;
           x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
+          if (!lz)  // recomputed w/q on a wide modulus: see below
+            x[k + half] = f64_red(x[k + half], q, qinv);
         }
         if (!(lz && (s & 1))) {  // lazy reduction: see inv_stages_f
 #pragma unroll
           for (int k = 0; k < E; k++)
             if (!(k & half))
+              x[k] = f64_red(x[k], q, qinv);
+        }
+        if (!W8 && !lz && s == LE - 1) {  // wide moduli: bounded products, see inv_stages_f
+#pragma unroll
+          for (int k = 0; k < E; k++)
+            if (k & half)
               x[k] = f64_red(x[k], q, qinv);
         }
       }
