@@ -1211,7 +1211,12 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
 static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)
 {
   check_ctx();
-  const size_t per = 65535 / nlimbs;
+  // groups of ~192 MiB: a group's column-pass output is still in the 256 MB
+  // Infinity Cache when its row pass reads it (config 2, 1024 polys x 8 limbs
+  // at N=2^16: roundtrip 8.41 -> 7.84 ms; 32-64 MiB groups lose more to
+  // launch gaps than they gain)
+  const size_t per = std::max<size_t>(1, std::min<size_t>(65535 / nlimbs, ((size_t)192 << 20) /
+                                                                              ((size_t)nlimbs * G.n * 8)));
   for (size_t p0 = 0; p0 < npolys; p0 += per) {
     const unsigned cnt = (unsigned)std::min(per, npolys - p0);
     k_ntt(qlimbs(data + p0 * nlimbs * G.n, nlimbs, cnt, (size_t)nlimbs * G.n), inverse);
