@@ -364,6 +364,68 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
   with_arith(q, m, logn, tw, [&](const auto &ar) { rows8_tile<LOGN2, INV>(ar, x, y, lds, n1 + row0); });
 }
 
+// Row pass of the batched NTT: a workgroup owns (basis slot, row tile) and a
+// range of polynomials; QN 256-thread quarters stream their own polys (the
+// next one's words prefetched) and share the tile's twiddles staged once in
+// LDS (RowTw; FP64 moduli forward and inverse from it, integer moduli the
+// forward ones), instead of every tile re-fetching its 20 twiddle pairs per
+// thread from L2.
+template <int LOGN2, bool INV, int QN>
+__global__ void __launch_bounds__(256 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+                                                             const ModConst *mcs, unsigned members)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];
+  __shared__ __attribute__((aligned(16))) uint64_t rtw[2 * RowTw<LOGN2>::ENTRIES];
+  const unsigned n1 = 1u << (logn - LOGN2), tiles = n1 / T::R, per = s.per, polys = s.count / per;
+  unsigned grp, mi;  // group = (slot, tile); members = poly ranges
+  if (!xcd_group(members, per * tiles, grp, mi))
+    return;
+  const unsigned pb0 = (unsigned)(((size_t)mi * polys) / members), pb1 = (unsigned)(((size_t)(mi + 1) * polys) / members);
+  if (pb0 >= pb1)
+    return;
+  const unsigned slot = grp / tiles, tile = grp % tiles, m = s.mod(slot);
+  const uint64_t q = mcs[m].q;
+  const unsigned row0 = tile * T::R;
+  const size_t toff = (size_t)row0 << LOGN2;
+  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  uint64_t *lq = rt[qi];
+  auto fetch = [&](uint64_t (&w)[8], unsigned p) {
+    const uint64_t *x = s.limb(p * per + slot, logn) + toff;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      w[k] = INV ? x[(th & ~63) * 8 + (th & 63) + 64 * k] : x[(row << LOGN2) + l + T::TA * k];
+  };
+  with_arith(q, m, logn, tw, [&](const auto &ar0) {
+    using A0 = std::decay_t<decltype(ar0)>;
+    constexpr bool F = std::is_same<A0, ArF64>::value;
+    // FP64: (w, w/q) of this direction; integer: the forward (w, w') pairs
+    RowTw<LOGN2>::stage(rtw, INV && F ? (const uint64_t *)ar0.itw : (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x,
+                        256 * QN);
+    __syncthreads();
+    const auto ar = [&] {
+      if constexpr (F)
+        return row_policy<LOGN2, false>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0), INV ? rtw : nullptr);
+      else
+        return row_policy<LOGN2, false>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0));
+    }();
+    unsigned p = pb0 + qi;
+    uint64_t nx[8];
+    if (p < pb1)
+      fetch(nx, p);
+    for (; p < pb1; p += QN) {
+      uint64_t w[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        w[k] = nx[k];
+      if (p + QN < pb1)
+        fetch(nx, p + QN);
+      wave_sync();
+      rows8_tile_words<LOGN2, INV>(ar, w, o.limb(p * per + slot, logn) + toff, lq, n1 + row0, th);
+    }
+  });
+}
+
 template <int LOGT1, int LOGN2>
 static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const uint64_t *post)
 {
@@ -371,6 +433,24 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const unsigned blocks = s.count * (n / 4096);
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const double pass_bytes = 16.0 * n * s.count;
+  // row pass: ntt_rows_q_kernel when every slot has polys enough to share
+  // a workgroup's staged twiddles, else one tile per workgroup
+  auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
+    constexpr int QN = 2;
+    const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
+    if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
+      const unsigned members = std::max(1u, polys / (4 * QN));  // ~4 polys per quarter
+      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN> : ntt_rows_q_kernel<LOGN2, false, QN>;
+      hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
+                         G.dev.mc, members);
+    } else if (inv) {
+      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
+                         G.dev.mc);
+    } else {
+      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn,
+                         tw, G.dev.mc);
+    }
+  };
   if (!inverse) {
     {
       ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
@@ -378,13 +458,11 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
                          G.dev.mc, (const uint64_t *)nullptr);
     }
     ProfScope ps(KC_NTT3_ROWS_FWD, pass_bytes);
-    hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, o, o, logn, tw,
-                       G.dev.mc);
+    rows_launch(false, o, o);
   } else {
     {
       ProfScope ps(KC_NTT3_ROWS_INV, pass_bytes);
-      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, s, o, logn, tw,
-                         G.dev.mc);
+      rows_launch(true, s, o);
     }
     ProfScope ps(KC_NTT2_COLS_INV, pass_bytes);
     hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,

@@ -361,7 +361,7 @@ struct ArF64Row : ArF64 {
   template <int LE>
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
-    if constexpr (!W8) {
+    if (!W8 && !itl) {  // (uniform) no staged inverse table: the global one
       ArF64::inv<LE>(x, bb, log_tlo);
     } else {
       constexpr int E = 1 << LE;
@@ -378,7 +378,7 @@ struct ArF64Row : ArF64 {
           const double U = x[k], V_ = x[k + half];
           x[k] = U + V_;
           x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
-          if (!lz)  // recomputed w/q on a wide modulus: see below
+          if (W8 && !lz)  // recomputed w/q on a wide modulus: see above
             x[k + half] = f64_red(x[k + half], q, qinv);
         }
         if (!(lz && (s & 1))) {  // lazy reduction: see inv_stages_f
@@ -670,11 +670,11 @@ __device__ __forceinline__ void rows8_fwd_raw(typename A::V (&r)[8], uint64_t *l
 
 template <int LOGN2, class A>
 __device__ __forceinline__ void rows8_fwd(typename A::V (&r)[8], uint64_t (&out)[8], uint64_t *lds, const A &ar,
-                                          uint64_t rowbase0)
+                                          uint64_t rowbase0, const int th = (int)threadIdx.x)
 {
   using T = Row8<LOGN2>;
   using V = typename A::V;
-  const int th = threadIdx.x, row = th / T::TA;
+  const int row = th / T::TA;
   const uint64_t rb = (rowbase0 + row) << LOGN2;
   {
     const int l = th % T::TA;
@@ -784,6 +784,48 @@ __device__ __forceinline__ void rows8_tile_raw(const A &ar, const uint64_t (&raw
 #pragma unroll
   for (int k = 0; k < 8; k++)
     y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+}
+
+// One row-pass tile from words the thread already holds (w: forward -- the
+// row-pass input words (row << LOGN2) + l + TA k, lazy; inverse -- the
+// coalesced words wl_elem(i), canonical), output canonical to y in the other
+// layout.  th: the thread's index in its 256-thread tile group.
+template <int LOGN2, bool INV, class A>
+__device__ __forceinline__ void rows8_tile_words(const A &ar, const uint64_t (&w)[8], uint64_t *y, uint64_t *lds,
+                                                 uint64_t rowbase0, const int th)
+{
+  using T = Row8<LOGN2>;
+  using V = typename A::V;
+  const int row = th / T::TA, h = th % T::TA, l = th % T::TA;
+  V r[8];
+  if constexpr (!INV) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::load_lazy(w[k]);
+    uint64_t out[8];
+    rows8_fwd<LOGN2>(r, out, lds, ar, rowbase0, th);
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      lds[T::at2(row, 8 * h, k)] = out[k];
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      y[(th & ~63) * 8 + (th & 63) + 64 * i] = lds[T::wl(th, i)];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      lds[T::wl(th, i)] = w[i];
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      r[k] = A::load(lds[T::at2(row, 8 * h, k)]);
+    wave_sync();
+    rows8_inv<LOGN2>(r, lds, ar, rowbase0, th);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+  }
 }
 
 template <int LOGN2, bool INV, class A>

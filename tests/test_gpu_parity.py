@@ -147,12 +147,15 @@ def test_evaluation_ops(oracle, product, name):
 
 
 @pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c14", "c15"])
-def test_ntt_batch_bitexact(oracle, product, name):
-    """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain on a
-    4-polynomial sample: forward, then inverse (the roundtrip identity)."""
+@pytest.mark.parametrize("npolys", [4, 24])
+def test_ntt_batch_bitexact(oracle, product, name, npolys):
+    """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain: forward, then
+    inverse (the roundtrip identity).  4 polys run the one-tile-per-workgroup
+    row pass; 24 the multi-poly row pass with staged twiddles (3 polys per
+    quarter stream, the next one prefetched)."""
     import torch
     init_both(oracle, product, name)
-    n, L, npolys = product.n, product.L, 4
+    n, L = product.n, product.L
     host = np.zeros(npolys * L * n, dtype=np.uint64)
     oracle.lib.poly_fill_uniform(host.ctypes.data, npolys, L, 99)
     orig = host.copy()
