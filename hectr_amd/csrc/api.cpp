@@ -148,12 +148,30 @@ static std::vector<PendEcd> g_pecd;
 static std::vector<int64_t> g_pcoef;  // n coefficients per pending encode
 static std::vector<PendEnc> g_penc;
 
+// he_gemv is queued the same way (at most two, run as one batch: the two
+// independent products of every control step of the caller, reference
+// src/hempc.c:255-262).  At any time only one of the two queues is non-empty:
+// he_gemv runs the encode/encrypt queue before queueing, and a deferred
+// encode / encryption runs the gemv queue first.
+struct PendGemv {
+  uint64_t *y;
+  size_t ypstride;
+  const uint64_t *x0, *x1;
+  const void *xdata;
+  unsigned lvl;
+  std::vector<GemvDiags> dgs;  // launches of up to GemvDiags::MAX diagonals; empty: all-zero matrix
+};
+static std::vector<PendGemv> g_pgemv;
+
 static void flush_pending();
+static void flush_gemvs();
 
 static void check_ctx()
 {
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
+  if (!g_pgemv.empty())
+    flush_gemvs();
   if (!g_pecd.empty() || !g_penc.empty())
     flush_pending();
 }
@@ -734,6 +752,8 @@ extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int s
   if (defer_ok(slots)) {
     // queued (flush_pending); a plaintext a queued encryption still reads, or
     // a queued encode target, is flushed first
+    if (!g_pgemv.empty())
+      flush_gemvs();
     bool busy = false;
     for (const PendEnc &e : g_penc)
       busy |= e.m == pt->data || e.c0 == pt->data;
@@ -788,6 +808,8 @@ extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
   const unsigned lvl = pt->nlimbs;
   if (defer_ok(0)) {
     // queued (flush_pending): streams taken now, in call order
+    if (!g_pgemv.empty())
+      flush_gemvs();
     bool busy = false;
     for (const PendEnc &e : g_penc)
       busy |= e.m == ct->data || e.c0 == ct->data;
@@ -1117,19 +1139,53 @@ static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
   return p;
 }
 
-extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
+// Runs the queued gemvs: ModUp of every input in one pass (one copy per
+// input, one INTT, one ModUp, one NTT over all digits), the inner products
+// per gemv, and one ModDown for each pair of outputs.  The arithmetic per
+// ciphertext is that of the unbatched sequence, so the results are too.
+static void flush_gemvs()
 {
-  check_ctx();
-  const unsigned lvl = x->nlimbs, s = G.slots;
-  if (lvl < 2)
-    gpqhe_die("he_gemv: input at the lowest level");
+  std::vector<PendGemv> q;
+  q.swap(g_pgemv);
+  if (q.empty())
+    return;
+  const unsigned k = (unsigned)q.size(), lvl = q[0].lvl;
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  const double *Md = (const double *)M;
+  Ws c1c((size_t)k * lvl * n), D((size_t)k * ndig * nm * n), acc((size_t)k * 2 * nm * n);
+  for (unsigned i = 0; i < k; i++)
+    HIP_CHECK(hipMemcpyAsync(c1c.p + (size_t)i * lvl * n, q[i].x1, (size_t)lvl * n * 8, hipMemcpyDeviceToDevice,
+                             G.stream));
+  k_ntt(qlimbs(c1c.p, lvl, k, lvl * n), true);
+  k_modup(D.p, c1c.p, k, lvl * n, (size_t)ndig * nm * n, lvl);
+  unsigned mods[GPQHE_MAXMOD];
+  basis_qp(lvl, mods);
+  k_ntt(limbset(D.p, mods, nm, k * ndig, nm * n), false);
+  for (unsigned i = 0; i < k; i++) {
+    uint64_t *a = acc.p + (size_t)i * 2 * nm * n;
+    bool started = false;
+    for (const GemvDiags &dg : q[i].dgs) {
+      k_gemv_inner(a, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1, lvl, dg, started);
+      started = true;
+    }
+    if (!started)  // all-zero matrix
+      HIP_CHECK(hipMemsetAsync(a, 0, 2 * nm * n * 8, G.stream));
+  }
+  if (k == 1)
+    k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 2, lvl, 1);
+  else
+    k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 4, lvl, 1, q[1].y);
+}
+
+// Unqueued he_gemv for matrices whose diagonals may overflow the cache: a
+// launch that refers to cached diagonals runs before the cache is cleared.
+static void gemv_now(he_ct_t *y, const double *Md, const he_ct_t *x, const he_evk_t rk[], unsigned lvl)
+{
+  const unsigned s = G.slots, nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n;
   Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
   hoist_modup(D.p, x, lvl);
   std::vector<double> diag(2 * (size_t)s);
-  // all non-zero diagonals in as few launches as possible (32 per launch)
   GemvDiags dg{};
   bool started = false;
   auto flush = [&]() {
@@ -1165,6 +1221,70 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     HIP_CHECK(hipMemsetAsync(acc.p, 0, 2 * nm * n * 8, G.stream));
   const double scale = x->scale;
   k_moddown(y->data, pstride(y), acc.p, nm * n, 2, lvl, 1);
+  y->nlimbs = lvl - 1;
+  y->scale = scale;
+  y->flags = 0;
+}
+
+extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
+{
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
+  if (!g_pecd.empty() || !g_penc.empty())
+    flush_pending();  // x may be a queued encryption
+  const unsigned lvl = x->nlimbs, s = G.slots;
+  if (lvl < 2)
+    gpqhe_die("he_gemv: input at the lowest level");
+  const double *Md = (const double *)M;
+  // queue behind the pending gemv only when the two are independent, at one
+  // level, with one output layout, and no diagonal encode can clear the
+  // cache the pending one refers to
+  static const bool defer = env_u("GPQHE_DEFER", 1) && env_u("GPQHE_DEFER_GEMV", 1);
+  const size_t dbytes = ((size_t)(lvl + G.K) << G.logn) * 8;
+  const bool may_clear = g_gemv_cache_bytes + (size_t)s * dbytes > ((size_t)1 << 31);
+  if (may_clear) {
+    // the diagonal cache may be cleared inside this call: unqueued form
+    flush_gemvs();
+    gemv_now(y, Md, x, rk, lvl);
+    return;
+  }
+  if (!g_pgemv.empty()) {
+    const PendGemv &p = g_pgemv.back();
+    if (g_pgemv.size() >= 2 || p.lvl != lvl || p.ypstride != pstride(y) || x->data == (void *)p.y ||
+        (const void *)y->data == p.xdata || y->data == p.y)
+      flush_gemvs();
+  }
+  PendGemv pg{y->data, pstride(y), limb(x, 0, 0), limb(x, 1, 0), x->data, lvl, {}};
+  std::vector<double> diag(2 * (size_t)s);
+  // all non-zero diagonals in as few launches as possible (GemvDiags::MAX each)
+  GemvDiags dg{};
+  for (unsigned d = 0; d < s; d++) {
+    bool nz = false;
+    for (unsigned i = 0; i < s; i++) {
+      const size_t src = (size_t)i * s + (i + d) % s;
+      diag[2 * i] = Md[2 * src];
+      diag[2 * i + 1] = Md[2 * src + 1];
+      nz |= diag[2 * i] != 0.0 || diag[2 * i + 1] != 0.0;
+    }
+    if (!nz)
+      continue;
+    const uint64_t *pt = diag_pt(diag.data(), s, lvl);
+    const uint64_t g = d == 0 ? 1 : galois_of_rot(d);
+    const he_evk_t *k = d == 0 ? nullptr : find_rot_key(rk, d, g);
+    dg.evk[dg.count] = k ? k->data : nullptr;
+    dg.pt[dg.count] = pt;
+    dg.g[dg.count] = g;
+    if (++dg.count == GemvDiags::MAX) {
+      pg.dgs.push_back(dg);
+      dg.count = 0;
+    }
+  }
+  if (dg.count)
+    pg.dgs.push_back(dg);
+  const double scale = x->scale;
+  g_pgemv.push_back(std::move(pg));
+  if (!defer)
+    flush_gemvs();
   y->nlimbs = lvl - 1;
   y->scale = scale;
   y->flags = 0;

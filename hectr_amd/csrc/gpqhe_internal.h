@@ -291,8 +291,9 @@ void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_strid
                 const uint64_t *evk, unsigned lvl, uint64_t g, const uint64_t *c0, const uint64_t *c1,
                 size_t c_stride, const uint64_t *pt, bool accumulate);
 // mode 0: divide by P; 1: by P q_{lvl-1}; 2: by q_{lvl-1} (X over q limbs only)
+// out2: the last nx_poly/2 outputs go there instead (see kernels.hip)
 void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned nx_poly,
-               unsigned lvl, int mode);
+               unsigned lvl, int mode, uint64_t *out2 = nullptr);
 void k_fill_uniform(uint64_t *data, size_t npolys, unsigned nlimbs, uint64_t seed);
 void k_mul_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);
 void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl, size_t pstride);

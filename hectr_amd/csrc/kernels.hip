@@ -2326,9 +2326,9 @@ __global__ void down_conv_kernel(uint64_t *conv, const uint64_t *X, unsigned log
 }
 
 // out[p][t] = (X[p][t] - conv[p][t]) * Dprod^-1
-__global__ void down_combine_kernel(uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                                    const uint64_t *conv, unsigned logn, unsigned lvl, unsigned L, DownTable tab,
-                                    const ModConst *mc)
+__global__ void down_combine_kernel(uint64_t *out, uint64_t *out2, unsigned half, size_t out_pstride,
+                                    const uint64_t *X, size_t x_pstride, const uint64_t *conv, unsigned logn,
+                                    unsigned lvl, unsigned L, DownTable tab, const ModConst *mc)
 {
   const size_t n = (size_t)1 << logn;
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2338,13 +2338,16 @@ __global__ void down_combine_kernel(uint64_t *out, size_t out_pstride, const uin
   const uint64_t q = mc[basis_mod(t, lvl, L)].q;
   const size_t o = ((size_t)t << logn) + k;
   const uint64_t v = sub_mod(X[p * x_pstride + o], conv[(((size_t)p * tab.keep + t) << logn) + k], q);
-  out[p * out_pstride + o] = mul_shoup(v, tab.dinv[t], tab.dinvp[t], q);
+  uint64_t *dst = p < half ? out + p * out_pstride : out2 + (p - half) * out_pstride;
+  dst[o] = mul_shoup(v, tab.dinv[t], tab.dinvp[t], q);
 }
 
 // X: npoly polynomials over basis_qp(lvl) (NTT domain, nm limbs each, stride
-// x_pstride); their drop limbs are overwritten (INTT in place).
+// x_pstride); their drop limbs are overwritten (INTT in place).  With out2,
+// the first npoly/2 results go to out and the rest to out2 (two ciphertexts
+// of one batched he_gemv flush).
 void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-               int mode)
+               int mode, uint64_t *out2)
 {
   DownTable &tab = down_table(lvl, mode);
   unsigned mods[GPQHE_MAXMOD];
@@ -2376,7 +2379,8 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
   k_ntt(cs, false);
   ProfScope ps(KC_DOWN_COMBINE, 8.0 * G.n * npoly * tab.keep * 3);
   hipLaunchKernelGGL(down_combine_kernel, dim3((G.n + TPB - 1) / TPB, tab.keep, npoly), dim3(TPB), 0, G.stream,
-                     out, out_pstride, X, x_pstride, conv, G.logn, lvl, G.L, tab, G.dev.mc);
+                     out, out2, out2 ? npoly / 2 : npoly, out_pstride, X, x_pstride, conv, G.logn, lvl, G.L, tab,
+                     G.dev.mc);
   HIP_CHECK(hipGetLastError());
   pool_free(conv);
 }
