@@ -315,7 +315,30 @@ def cstr_loop(steps):
     rel = float(max(np.max(np.abs(x - xp) / np.abs(xp)), np.max(np.abs(u - up) / np.abs(up))))
     return {"steps": steps, "horizon": pb.horizon, "slots": pb.slots, "steps_per_s": steps / dt,
             "regulator_ms_median": 1e3 * float(np.median(reg.timings)), "keygen_s": reg.keygen_s,
-            "max_rel_dev_vs_plaintext": rel}
+            "max_rel_dev_vs_plaintext": rel, "c_caller": cstr_c_caller()}
+
+
+def cstr_c_caller(reps=3):
+    """HECTR's own unchanged harness (`test-hectr cstr-hempc`: 40 steps, C
+    caller, its pmu timer around the closed loop) on the product library, as a
+    child process; present when the binary was built in the build container
+    (oracle/_ref, `make -C harness hectr`)."""
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "_ref", "test-hectr")
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "hectr_amd", "lib"), GPQHE_SEED="5")
+    ms = []
+    for _ in range(reps):
+        with tempfile.TemporaryDirectory() as d:
+            os.makedirs(os.path.join(d, "results"))
+            r = subprocess.run([exe, "cstr-hempc"], cwd=d, env=env, capture_output=True, text=True, timeout=120)
+            m = re.search(r"closed-loop simulate\s+([0-9.]+) ms", r.stdout + r.stderr)
+            if r.returncode or not m:
+                return {"error": (r.stdout + r.stderr)[-300:]}
+            ms.append(float(m.group(1)))
+    med = sorted(ms)[len(ms) // 2]
+    return {"steps": 40, "closed_loop_ms_median": med, "steps_per_s": 40e3 / med, "runs_ms": ms}
 
 
 def usable_cpus():
