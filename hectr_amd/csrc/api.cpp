@@ -221,7 +221,10 @@ static unsigned basis_qp(unsigned lvl, unsigned *mods)
 
 static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
 {
-  check_ctx();
+  // no flush of the queued work: a fresh block cannot alias a live object
+  // that queued work refers to (objects are flushed before they are freed)
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
   he_ct_t *o = OB(vo);
   memset(o, 0, sizeof(*o));
   o->npoly = npoly;
@@ -787,11 +790,14 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
   const unsigned nl = pt->nlimbs;
   const size_t words = (size_t)nl << G.logn;
   Ws c(words);
-  HIP_CHECK(hipMemcpyAsync(c.p, pt->data, words * 8, hipMemcpyDeviceToDevice, G.stream));
-  if (!(pt->flags & GPQHE_F_COEFF))
-    k_ntt(qlimbs(c.p, nl, 1, words), true);
+  const uint64_t *src = pt->data;
+  if (!(pt->flags & GPQHE_F_COEFF)) {
+    // out-of-place inverse transform (the plaintext stays in NTT form)
+    k_ntt_ex(qlimbs(pt->data, nl, 1, words), qlimbs(c.p, nl, 1, words), true, nullptr);
+    src = c.p;
+  }
   std::vector<uint64_t> host(words);
-  HIP_CHECK(hipMemcpyAsync(host.data(), c.p, words * 8, hipMemcpyDeviceToHost, G.stream));
+  HIP_CHECK(hipMemcpyAsync(host.data(), src, words * 8, hipMemcpyDeviceToHost, G.stream));
   HIP_CHECK(hipStreamSynchronize(G.stream));
   hm_decode((double *)z, host.data(), nl, slots, G.n, pt->scale);
 }
@@ -1062,15 +1068,10 @@ static const he_evk_t *find_rot_key(const he_evk_t rk[], unsigned r, uint64_t g)
 // c1 of x -> coefficient domain -> ModUp digits (NTT domain) in D.
 static void hoist_modup(uint64_t *D, const he_ct_t *x, unsigned lvl)
 {
-  const size_t n = G.n;
-  Ws c1c((size_t)lvl * n);
-  HIP_CHECK(hipMemcpyAsync(c1c.p, limb(x, 1, 0), (size_t)lvl * n * 8, hipMemcpyDeviceToDevice, G.stream));
-  k_ntt(qlimbs(c1c.p, lvl, 1, lvl * n), true);
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
-  k_modup(D, c1c.p, 1, lvl * n, (size_t)ndig * nm * n, lvl);
-  unsigned mods[GPQHE_MAXMOD];
-  basis_qp(lvl, mods);
-  k_ntt(limbset(D, mods, nm, ndig, nm * n), false);
+  XPtrs x1{};
+  x1.p[0] = limb(x, 1, 0);
+  k_modup_ntt(D, x1, 1, (size_t)ndig * nm * G.n, lvl);
 }
 
 extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const he_evk_t rk[])
@@ -1139,9 +1140,9 @@ static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
   return p;
 }
 
-// Runs the queued gemvs: ModUp of every input in one pass (one copy per
-// input, one INTT, one ModUp, one NTT over all digits), the inner products
-// per gemv, and one ModDown for each pair of outputs.  The arithmetic per
+// Runs the queued gemvs: ModUp of every input in one pass (k_modup_ntt: one
+// fused launch at n <= 2^12), the inner products per gemv, and one ModDown
+// for each pair of outputs.  The arithmetic per
 // ciphertext is that of the unbatched sequence, so the results are too.
 static void flush_gemvs()
 {
@@ -1152,24 +1153,32 @@ static void flush_gemvs()
   const unsigned k = (unsigned)q.size(), lvl = q[0].lvl;
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  Ws c1c((size_t)k * lvl * n), D((size_t)k * ndig * nm * n), acc((size_t)k * 2 * nm * n);
+  Ws D((size_t)k * ndig * nm * n), acc((size_t)k * 2 * nm * n);
+  XPtrs x1{};
   for (unsigned i = 0; i < k; i++)
-    HIP_CHECK(hipMemcpyAsync(c1c.p + (size_t)i * lvl * n, q[i].x1, (size_t)lvl * n * 8, hipMemcpyDeviceToDevice,
-                             G.stream));
-  k_ntt(qlimbs(c1c.p, lvl, k, lvl * n), true);
-  k_modup(D.p, c1c.p, k, lvl * n, (size_t)ndig * nm * n, lvl);
-  unsigned mods[GPQHE_MAXMOD];
-  basis_qp(lvl, mods);
-  k_ntt(limbset(D.p, mods, nm, k * ndig, nm * n), false);
-  for (unsigned i = 0; i < k; i++) {
-    uint64_t *a = acc.p + (size_t)i * 2 * nm * n;
-    bool started = false;
-    for (const GemvDiags &dg : q[i].dgs) {
-      k_gemv_inner(a, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1, lvl, dg, started);
-      started = true;
+    x1.p[i] = q[i].x1;
+  k_modup_ntt(D.p, x1, k, (size_t)ndig * nm * n, lvl);
+  // every gemv with one launch's worth of diagonals: all in one launch
+  bool one = k <= GemvJobs::MAX;
+  for (unsigned i = 0; i < k; i++)
+    one &= q[i].dgs.size() == 1;
+  if (one) {
+    GemvJobs jobs;
+    for (unsigned i = 0; i < k; i++)
+      jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1,
+                          q[i].dgs[0], 0};
+    k_gemv_inner_jobs(jobs, k, lvl);
+  } else {
+    for (unsigned i = 0; i < k; i++) {
+      uint64_t *a = acc.p + (size_t)i * 2 * nm * n;
+      bool started = false;
+      for (const GemvDiags &dg : q[i].dgs) {
+        k_gemv_inner(a, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1, lvl, dg, started);
+        started = true;
+      }
+      if (!started)  // all-zero matrix
+        HIP_CHECK(hipMemsetAsync(a, 0, 2 * nm * n * 8, G.stream));
     }
-    if (!started)  // all-zero matrix
-      HIP_CHECK(hipMemsetAsync(a, 0, 2 * nm * n * 8, G.stream));
   }
   if (k == 1)
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 2, lvl, 1);

@@ -247,6 +247,9 @@ void pool_release_all();
 // Kernel launchers (kernels.hip)
 // ---------------------------------------------------------------------------
 void k_ntt(const LimbSet &s, bool inverse);
+// out of place (in and out of the same geometry; out may equal in); post: per-slot
+// Shoup pairs replacing n^-1 (inverse only, n >= 2^13)
+void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_t *post);
 void k_binop(uint64_t *out, const uint64_t *a, const uint64_t *b, unsigned npoly, unsigned lvl,
              size_t out_pstride, size_t a_pstride, size_t b_pstride, int op);
 void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t pstride);
@@ -276,6 +279,11 @@ void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint
 void k_automorph(uint64_t *out, const uint64_t *in, unsigned nlimbs, uint64_t g);
 void k_square(uint64_t *out, const uint64_t *in, unsigned nlimbs);
 void k_modup(uint64_t *D, const uint64_t *xc, unsigned count, size_t x_stride, size_t d_stride, unsigned lvl);
+struct XPtrs {
+  static constexpr unsigned MAX = 8;
+  const uint64_t *p[MAX];
+};
+void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, unsigned lvl);
 // acc [count][2][lvl+K][n] (stride acc_stride): acc0 then acc1
 // he_gemv diagonals of one launch (passed by value as kernel arguments)
 struct GemvDiags {
@@ -287,6 +295,17 @@ struct GemvDiags {
 };
 void k_gemv_inner(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1, unsigned lvl,
                   const GemvDiags &dg, bool accumulate);
+struct GemvJob {
+  uint64_t *acc;
+  const uint64_t *D, *x0, *x1;
+  GemvDiags dg;
+  int accumulate;
+};
+struct GemvJobs {
+  static constexpr unsigned MAX = 2;  // kernel arguments: ~0.8 KB per job
+  GemvJob j[MAX];
+};
+void k_gemv_inner_jobs(const GemvJobs &jobs, unsigned njobs, unsigned lvl);
 void k_ks_inner(uint64_t *acc, const uint64_t *D, unsigned count, size_t d_stride, size_t acc_stride,
                 const uint64_t *evk, unsigned lvl, uint64_t g, const uint64_t *c0, const uint64_t *c1,
                 size_t c_stride, const uint64_t *pt, bool accumulate);

@@ -42,7 +42,7 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
   KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
-  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP, KC_COUNT
+  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP, KC_MODUP_SMALL, KC_DOWN_SMALL, KC_COUNT
 };
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
@@ -51,7 +51,7 @@ static const char *kc_names[KC_COUNT] = {
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "dn_cols_kernel", "dn_rows_kernel",
   "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
-  "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>"};
+  "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>", "modup_small_kernel", "moddown_small_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -479,10 +479,16 @@ static bool ntt2_ok()
 
 // Out-of-place NTT (in and out have the same geometry; out may equal in);
 // `post` (inverse only) replaces n^-1 by per-slot Shoup pairs post[2 (v % per)].
+static void ntt_small_launch(const LimbSet &s, const LimbSet &in, bool inverse);
+
 void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_t *post)
 {
   if (!in.count)
     return;
+  if (G.logn >= 10 && G.logn <= 12 && !post) {
+    ntt_small_launch(out, in.base == out.base && !in.ngp ? LimbSet{} : in, inverse);
+    return;
+  }
   switch (G.logn) {
   case 13: ntt2_launch<6, 7>(in, out, inverse, post); return;
   case 14: ntt2_launch<7, 7>(in, out, inverse, post); return;
@@ -510,110 +516,132 @@ __device__ __forceinline__ uint64_t lift_i64(int64_t v, const ModConst &c)
   return r == c.q ? 0 : c.q - r;
 }
 
+// The rounds as device functions: the first loads and the last stores are the
+// caller's (load(k, i) -> V, store(k, i, V) for element i held in slot k).
+// The last inverse round and the first forward round both give thread th the
+// elements th + k n/8 (k < 8), so a caller can finish an inverse transform,
+// combine per element in registers and start a forward transform on the
+// result without an LDS pass (modup_small_kernel, moddown_small_kernel).
+template <int LOGN, class A, class LD, class ST>
+__device__ __forceinline__ void small_fwd(const A &ar, uint64_t *lds, LD &&load, ST &&store)
+{
+  using V = typename A::V;
+  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
+  const int th = threadIdx.x;
+  V a[8];
+#pragma unroll
+  for (int r = 0; r < FULL; r++) {
+    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = r ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
+    ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
+    if (r + 1 < FULL || REM) {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        lds[pos0 + k * d8] = A::bits(a[k]);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        store(k, pos0 + k * d8, a[k]);
+    }
+  }
+  if constexpr (REM > 0) {
+    // last REM stages (distances 2^(REM-1) .. 1): thread t owns 8
+    // consecutive elements = 8 / 2^REM groups
+    constexpr int EG = 1 << REM;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = A::unbits(lds[8 * th + k]);
+#pragma unroll
+    for (int j = 0; j < 8 / EG; j++) {
+      V g[EG];
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        g[e] = a[j * EG + e];
+      ar.template fwd<REM>(g, (uint64_t)n + 8 * th + EG * j, REM - 1);
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        store(j * EG + e, 8 * th + j * EG + e, g[e]);
+    }
+  }
+}
+
+template <int LOGN, class A, class LD, class ST>
+__device__ __forceinline__ void small_inv(const A &ar, uint64_t *lds, LD &&load, ST &&store)
+{
+  using V = typename A::V;
+  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
+  const int th = threadIdx.x;
+  V a[8];
+  if constexpr (REM > 0) {
+    constexpr int EG = 1 << REM;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = load(k, 8 * th + k);
+#pragma unroll
+    for (int j = 0; j < 8 / EG; j++) {
+      V g[EG];
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        g[e] = a[j * EG + e];
+      ar.template inv<REM>(g, (uint64_t)n + 8 * th + EG * j, 0);
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        lds[8 * th + j * EG + e] = A::bits(g[e]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int rr = 0; rr < FULL; rr++) {
+    const int r = FULL - 1 - rr;  // smallest distances first
+    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = (rr || REM) ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
+    ar.template inv<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 3);
+    if (rr + 1 < FULL) {
+      __syncthreads();  // every group of this round has read its inputs
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        lds[pos0 + k * d8] = A::bits(a[k]);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        store(k, pos0 + k * d8, a[k]);
+    }
+  }
+}
+
 template <int LOGN, bool INV>
 __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs,
-                                                         const int64_t *coef)
+                                                         const int64_t *coef, LimbSet in)
 {
-  constexpr int n = 1 << LOGN, NT = n / 8, FULL = LOGN / 3, REM = LOGN % 3;
+  constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
   const unsigned v = blockIdx.x;
   uint64_t *x = s.limb(v, LOGN);
+  const uint64_t *xi = in.base ? in.limb(v, LOGN) : x;  // out of place: same geometry
   const unsigned m = s.mod(v);
   const ModConst mc = mcs[m];
-  const int th = threadIdx.x;
   with_arith(mc.q, m, LOGN, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
     using V = typename A::V;
-    // elements of a radix-8 group of round r (distances n>>(3r+1) .. n>>(3r+3))
-    auto group = [&](int r, int &pos0, int &d8) {
-      d8 = n >> (3 * r + 3);
-      pos0 = (th / d8) * 8 * d8 + th % d8;
-    };
-    V a[8];
     if constexpr (!INV) {
-#pragma unroll
-      for (int r = 0; r < FULL; r++) {
-        int pos0, d8;
-        group(r, pos0, d8);
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          a[k] = r ? A::unbits(lds[pos0 + k * d8])
-                   : A::load(coef ? lift_i64(coef[((size_t)(v / s.per) << LOGN) + pos0 + k * d8], mc)
-                                  : x[pos0 + k * d8]);
-        ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
-        if (r + 1 < FULL || REM) {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            lds[pos0 + k * d8] = A::bits(a[k]);
-          __syncthreads();
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            x[pos0 + k * d8] = ar.canon(a[k]);
-        }
-      }
-      if constexpr (REM > 0) {
-        // last REM stages (distances 2^(REM-1) .. 1): thread t owns 8
-        // consecutive elements = 8 / 2^REM groups
-        constexpr int EG = 1 << REM;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          a[k] = A::unbits(lds[8 * th + k]);
-#pragma unroll
-        for (int j = 0; j < 8 / EG; j++) {
-          V g[EG];
-#pragma unroll
-          for (int e = 0; e < EG; e++)
-            g[e] = a[j * EG + e];
-          ar.template fwd<REM>(g, (uint64_t)n + 8 * th + EG * j, REM - 1);
-#pragma unroll
-          for (int e = 0; e < EG; e++)
-            x[8 * th + j * EG + e] = ar.canon(g[e]);
-        }
-      }
+      small_fwd<LOGN>(
+          ar, lds,
+          [&](int, int i) {
+            return A::load(coef ? lift_i64(coef[((size_t)(v / s.per) << LOGN) + i], mc) : xi[i]);
+          },
+          [&](int, int i, V a) { x[i] = ar.canon(a); });
     } else {
-      if constexpr (REM > 0) {
-        constexpr int EG = 1 << REM;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          a[k] = A::load(x[8 * th + k]);
-#pragma unroll
-        for (int j = 0; j < 8 / EG; j++) {
-          V g[EG];
-#pragma unroll
-          for (int e = 0; e < EG; e++)
-            g[e] = a[j * EG + e];
-          ar.template inv<REM>(g, (uint64_t)n + 8 * th + EG * j, 0);
-#pragma unroll
-          for (int e = 0; e < EG; e++)
-            lds[8 * th + j * EG + e] = A::bits(g[e]);
-        }
-        __syncthreads();
-      }
-#pragma unroll
-      for (int rr = 0; rr < FULL; rr++) {
-        const int r = FULL - 1 - rr;  // smallest distances first
-        int pos0, d8;
-        group(r, pos0, d8);
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          a[k] = (rr || REM) ? A::unbits(lds[pos0 + k * d8]) : A::load(x[pos0 + k * d8]);
-        ar.template inv<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 3);
-        if (rr + 1 < FULL) {
-          __syncthreads();  // every group of this round has read its inputs
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            lds[pos0 + k * d8] = A::bits(a[k]);
-          __syncthreads();
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            x[pos0 + k * d8] = ar.mulc(a[k], mc.ninv, mc.ninvp);
-        }
-      }
+      small_inv<LOGN>(
+          ar, lds, [&](int, int i) { return A::load(xi[i]); },
+          [&](int, int i, V a) { x[i] = ar.mulc(a, mc.ninv, mc.ninvp); });
     }
   });
-  (void)NT;
 }
 
 // Encoding: lift the signed coefficients into every limb of s, then the
@@ -624,7 +652,7 @@ void k_lift_ntt(const LimbSet &s, const int64_t *coef)
     ProfScope ps(KC_NTT_SMALL_FWD, 8.0 * G.n * (s.count + 1));
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern, unsigned threads) {
-      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, coef);
+      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, coef, LimbSet{});
     };
     if (G.logn == 12)
       go(ntt_small_kernel<12, false>, 512);
@@ -639,6 +667,26 @@ void k_lift_ntt(const LimbSet &s, const int64_t *coef)
   k_ntt(s, false);
 }
 
+// ntt_small_kernel over s; `in` (same geometry, base != nullptr): read the
+// input from there (out of place).
+static void ntt_small_launch(const LimbSet &s, const LimbSet &in, bool inverse)
+{
+  const unsigned logn = G.logn, n = G.n;
+  ProfScope ps(inverse ? KC_NTT_SMALL_INV : KC_NTT_SMALL_FWD, 16.0 * n * s.count);
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  auto go = [&](auto kern, unsigned threads) {
+    hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, (const int64_t *)nullptr,
+                       in);
+  };
+  if (logn == 12)
+    inverse ? go(ntt_small_kernel<12, true>, 512) : go(ntt_small_kernel<12, false>, 512);
+  else if (logn == 11)
+    inverse ? go(ntt_small_kernel<11, true>, 256) : go(ntt_small_kernel<11, false>, 256);
+  else
+    inverse ? go(ntt_small_kernel<10, true>, 128) : go(ntt_small_kernel<10, false>, 128);
+  HIP_CHECK(hipGetLastError());
+}
+
 void k_ntt(const LimbSet &s, bool inverse)
 {
   if (!s.count)
@@ -647,18 +695,7 @@ void k_ntt(const LimbSet &s, bool inverse)
   if (s.count > 65535)
     gpqhe_die("k_ntt: %u limbs in one launch", s.count);
   if (logn >= 10 && logn <= 12) {
-    ProfScope ps(inverse ? KC_NTT_SMALL_INV : KC_NTT_SMALL_FWD, 16.0 * n * s.count);
-    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
-    auto go = [&](auto kern, unsigned threads) {
-      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, (const int64_t *)nullptr);
-    };
-    if (logn == 12)
-      inverse ? go(ntt_small_kernel<12, true>, 512) : go(ntt_small_kernel<12, false>, 512);
-    else if (logn == 11)
-      inverse ? go(ntt_small_kernel<11, true>, 256) : go(ntt_small_kernel<11, false>, 256);
-    else
-      inverse ? go(ntt_small_kernel<10, true>, 128) : go(ntt_small_kernel<10, false>, 128);
-    HIP_CHECK(hipGetLastError());
+    ntt_small_launch(s, LimbSet{}, inverse);
     return;
   }
   if (logn <= 12) {
@@ -1484,12 +1521,17 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
 // A block covers 32 coefficients of one basis slot with 8 diagonal lanes
 // (thread (c, g) sums diagonals g, g + 8, ...); the 8 partial sums meet in
 // LDS.  grid: (n / 32, nm), 256 threads.
-__global__ void __launch_bounds__(256) gemv_inner_kernel(uint64_t *acc, const uint64_t *D, const uint64_t *x0,
-                                                          const uint64_t *x1, unsigned logn, unsigned lvl,
-                                                          unsigned L, unsigned nm, unsigned nmod, unsigned ndig,
-                                                          GemvDiags dg, int accumulate, const ModConst *mc)
+__global__ void __launch_bounds__(256) gemv_inner_kernel(GemvJobs jobs, unsigned logn, unsigned lvl, unsigned L,
+                                                          unsigned nm, unsigned nmod, unsigned ndig,
+                                                          const ModConst *mc)
 {
   __shared__ uint64_t part[2][8][32];
+  // blockIdx.z: the job (gemvs queued together run in one launch)
+  const GemvJob &job = jobs.j[blockIdx.z];
+  uint64_t *acc = job.acc;
+  const uint64_t *D = job.D, *x0 = job.x0, *x1 = job.x1;
+  const GemvDiags &dg = job.dg;
+  const int accumulate = job.accumulate;
   const unsigned c = threadIdx.x % 32, gl = threadIdx.x / 32;
   const size_t k = (size_t)blockIdx.x * 32 + c;
   const unsigned t = blockIdx.y;
@@ -1531,14 +1573,26 @@ __global__ void __launch_bounds__(256) gemv_inner_kernel(uint64_t *acc, const ui
   }
 }
 
+void k_gemv_inner_jobs(const GemvJobs &jobs, unsigned njobs, unsigned lvl)
+{
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  if (njobs < 1 || njobs > GemvJobs::MAX)
+    gpqhe_die("k_gemv_inner_jobs: %u jobs", njobs);
+  double diags = 0;
+  for (unsigned i = 0; i < njobs; i++)
+    diags += jobs.j[i].dg.count;
+  ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * diags * (ndig * nm + 2 * nm + 2 * lvl));
+  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 32, nm, njobs), dim3(256), 0, G.stream, jobs, G.logn, lvl, G.L,
+                     nm, G.nmod, ndig, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
 void k_gemv_inner(uint64_t *acc, const uint64_t *D, const uint64_t *x0, const uint64_t *x1, unsigned lvl,
                   const GemvDiags &dg, bool accumulate)
 {
-  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
-  ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * (double)dg.count * (ndig * nm + 2 * nm + 2 * lvl));
-  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 32, nm), dim3(256), 0, G.stream, acc, D, x0, x1, G.logn, lvl,
-                     G.L, nm, G.nmod, ndig, dg, accumulate ? 1 : 0, G.dev.mc);
-  HIP_CHECK(hipGetLastError());
+  GemvJobs jobs;
+  jobs.j[0] = GemvJob{acc, D, x0, x1, dg, accumulate ? 1 : 0};
+  k_gemv_inner_jobs(jobs, 1, lvl);
 }
 
 // acc layout per ciphertext p: acc0 at acc + p*acc_stride, acc1 right after
@@ -2342,6 +2396,176 @@ __global__ void down_combine_kernel(uint64_t *out, uint64_t *out2, unsigned half
   dst[o] = mul_shoup(v, tab.dinv[t], tab.dinvp[t], q);
 }
 
+// Fused small-N ModUp (n = 2^10 .. 2^12): digit j of c1 (NTT domain, x[p]) to
+// basis slot t, in one workgroup: the inverse transform of each of the
+// digit's limbs, its products y_i = x_i [(Q_j/q_i)^-1] and the sum
+// sum_i y_i [Q_j/q_i]_t (128-bit, one REDC) in registers, then the forward
+// transform mod q_t.  The digit's own slots are the input limbs themselves.
+// Replaces copy + INTT + modup_kernel + NTT (four launches) with one; every
+// value equals theirs (canonical residues at each step).
+// grid: (nm, ndig, count), n / 8 threads.
+template <int LOGN>
+__global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1, size_t d_stride, unsigned lvl,
+                                                           unsigned L, unsigned nm, Tw2 tw, UpTable tab,
+                                                           const ModConst *mcs)
+{
+  constexpr int n = 1 << LOGN;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned t = blockIdx.x, j = blockIdx.y, p = blockIdx.z;
+  const UpDigit *dg = tab.dig + j;
+  const unsigned lo = dg->lo, na = dg->na;
+  const uint64_t *x = x1.p[p];
+  uint64_t *out = D + p * d_stride + (((size_t)j * nm + t) << LOGN);
+  const int th = threadIdx.x;
+  if (t >= lo && t < lo + na) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      out[th + k * (n / 8)] = x[((size_t)t << LOGN) + th + k * (n / 8)];
+    return;
+  }
+  unsigned __int128 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    acc[k] = 0;
+  const uint64_t *cj = tab.c + (size_t)j * 8 * nm;
+  for (unsigned i = 0; i < na; i++) {
+    const unsigned ms = lo + i;
+    const ModConst mc = mcs[ms];
+    const uint64_t *src = x + ((size_t)ms << LOGN);
+    const uint64_t cw = cj[i * nm + t], yw = dg->y[i], ywp = dg->yp[i];
+    if (i)
+      __syncthreads();
+    with_arith(mc.q, ms, LOGN, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      small_inv<LOGN>(
+          ar, lds, [&](int, int e) { return A::load(src[e]); },
+          [&](int k, int, typename A::V a) {
+            const uint64_t y = mul_shoup(ar.mulc(a, mc.ninv, mc.ninvp), yw, ywp, mc.q);
+            acc[k] += (unsigned __int128)y * cw;
+          });
+    });
+  }
+  __syncthreads();
+  const unsigned mt = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[mt];
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = redc128((uint64_t)(acc[k] >> 64), (uint64_t)acc[k], mc);
+  with_arith(mc.q, mt, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds, [&](int k, int) { return A::load(r[k]); },
+        [&](int, int e, typename A::V a) { out[e] = ar.canon(a); });
+  });
+}
+
+// Fused small-N ModDown (+ rescale by its mode): output slot t of poly p in
+// one workgroup: the inverse transform of each dropped limb, the conversion
+// sum in registers, the forward transform mod q_t, and
+// out = (X[t] - conv) [D^-1]_t.  Replaces INTT + down_conv + NTT +
+// down_combine; X is only read (the in-place call of he_rescale is safe: each
+// output word is written by the thread that read X at that word).
+// grid: (keep, npoly), n / 8 threads.
+template <int LOGN>
+__global__ void __launch_bounds__(512) moddown_small_kernel(uint64_t *out, uint64_t *out2, unsigned half,
+                                                             size_t out_pstride, const uint64_t *X, size_t x_pstride,
+                                                             unsigned lvl, unsigned L, Tw2 tw, DownTable tab,
+                                                             const ModConst *mcs)
+{
+  __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN];
+  const unsigned t = blockIdx.x, p = blockIdx.y;
+  const uint64_t *x = X + p * x_pstride;
+  unsigned __int128 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    acc[k] = 0;
+  for (unsigned d = 0; d < tab.nd; d++) {
+    const unsigned bd = tab.keep + d, md = basis_mod(bd, lvl, L);
+    const ModConst mc = mcs[md];
+    const uint64_t *src = x + ((size_t)bd << LOGN);
+    const uint64_t cw = tab.c[(size_t)d * tab.keep + t], yw = tab.y[d], ywp = tab.yp[d];
+    if (d)
+      __syncthreads();
+    with_arith(mc.q, md, LOGN, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      small_inv<LOGN>(
+          ar, lds, [&](int, int e) { return A::load(src[e]); },
+          [&](int k, int, typename A::V a) {
+            const uint64_t y = mul_shoup(ar.mulc(a, mc.ninv, mc.ninvp), yw, ywp, mc.q);
+            acc[k] += (unsigned __int128)y * cw;
+          });
+    });
+  }
+  __syncthreads();
+  const unsigned mt = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[mt];
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = redc128((uint64_t)(acc[k] >> 64), (uint64_t)acc[k], mc);
+  const uint64_t *xt = x + ((size_t)t << LOGN);
+  uint64_t *dst = (p < half ? out + p * out_pstride : out2 + (p - half) * out_pstride) + ((size_t)t << LOGN);
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t];
+  with_arith(mc.q, mt, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds, [&](int k, int) { return A::load(r[k]); },
+        [&](int, int e, typename A::V a) {
+          dst[e] = mul_shoup(sub_mod(xt[e], ar.canon(a), mc.q), dinv, dinvp, mc.q);
+        });
+  });
+}
+
+// ModUp of NTT-domain inputs x1.p[0..count) (lvl limbs each, e.g. c1 of a
+// ciphertext, left unchanged) into D [count][ndig][nm] (NTT domain): one fused
+// launch for n <= 2^12, else copy + INTT + modup_kernel + NTT.
+void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, unsigned lvl)
+{
+  UpTable &tab = up_table(lvl);
+  const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
+  if (count > XPtrs::MAX)
+    gpqhe_die("k_modup_ntt: %u inputs (max %u)", count, XPtrs::MAX);
+  if (G.logn >= 10 && G.logn <= 12) {
+    ProfScope ps(KC_MODUP_SMALL, 8.0 * n * count * ((double)ndig * lvl + ndig * nm));
+    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(nm, ndig, count), dim3(n / 8), 0, G.stream, D, x1, d_stride, lvl, G.L, nm, tw,
+                         tab, G.dev.mc);
+    };
+    if (G.logn == 12)
+      go(modup_small_kernel<12>);
+    else if (G.logn == 11)
+      go(modup_small_kernel<11>);
+    else
+      go(modup_small_kernel<10>);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const size_t w = (size_t)lvl * n;
+  uint64_t *c1c = (uint64_t *)pool_alloc((size_t)count * w * 8);
+  for (unsigned i = 0; i < count; i++)
+    HIP_CHECK(hipMemcpyAsync(c1c + i * w, x1.p[i], w * 8, hipMemcpyDeviceToDevice, G.stream));
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned l = 0; l < lvl; l++)
+    mods[l] = l;
+  auto limbs = [](uint64_t *base, const unsigned *md, unsigned per, unsigned groups, size_t stride) {
+    LimbSet ls{};
+    ls.base = base;
+    ls.per = per;
+    ls.count = per * groups;
+    ls.stride = stride;
+    for (unsigned i = 0; i < per; i++)
+      ls.mods[i] = (uint8_t)md[i];
+    return ls;
+  };
+  k_ntt(limbs(c1c, mods, lvl, count, w), true);
+  k_modup(D, c1c, count, w, d_stride, lvl);
+  basis_qp(lvl, mods);
+  k_ntt(limbs(D, mods, nm, count * ndig, (size_t)nm * n), false);
+  pool_free(c1c);
+}
+
 // X: npoly polynomials over basis_qp(lvl) (NTT domain, nm limbs each, stride
 // x_pstride); their drop limbs are overwritten (INTT in place).  With out2,
 // the first npoly/2 results go to out and the rest to out2 (two ciphertexts
@@ -2350,6 +2574,24 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
                int mode, uint64_t *out2)
 {
   DownTable &tab = down_table(lvl, mode);
+  if (G.logn >= 10 && G.logn <= 12) {
+    // one fused launch (moddown_small_kernel)
+    ProfScope ps(KC_DOWN_SMALL, 8.0 * G.n * npoly * (tab.nd + 2.0 * tab.keep));
+    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+    const unsigned half = out2 ? npoly / 2 : npoly;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, X,
+                         x_pstride, lvl, G.L, tw, tab, G.dev.mc);
+    };
+    if (G.logn == 12)
+      go(moddown_small_kernel<12>);
+    else if (G.logn == 11)
+      go(moddown_small_kernel<11>);
+    else
+      go(moddown_small_kernel<10>);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   unsigned mods[GPQHE_MAXMOD];
   basis_qp(lvl, mods);
   LimbSet ds{};

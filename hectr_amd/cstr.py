@@ -341,9 +341,8 @@ class EncryptedRegulator:
         t0 = time.perf_counter()
         # hectr_enc_states (src/ctr.c:445-481): encode + encrypt 5 vectors
         vals = {"up": np.zeros(s), "xhat": xhat, "uhat": uhat, "xr": xr, "ur": ur}
-        pts = {}
+        pts = {k: e.pt() for k in ("up", "xhat", "uhat", "xr", "ur")}  # src/ctr.c:461-465
         for k in ("up", "xhat", "uhat", "xr", "ur"):
-            pts[k] = e.pt()
             e.ecd(pts[k], d2z_vector(vals[k], s))
         for k in ("up", "xhat", "uhat", "xr", "ur"):
             e.enc_pk(c[k], pts[k], self.pk)
