@@ -328,17 +328,28 @@ def cstr_c_caller(reps=3):
     if not os.path.exists(exe):
         return None
     env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "hectr_amd", "lib"), GPQHE_SEED="5")
-    ms = []
-    for _ in range(reps):
-        with tempfile.TemporaryDirectory() as d:
-            os.makedirs(os.path.join(d, "results"))
-            r = subprocess.run([exe, "cstr-hempc"], cwd=d, env=env, capture_output=True, text=True, timeout=120)
-            m = re.search(r"closed-loop simulate\s+([0-9.]+) ms", r.stdout + r.stderr)
-            if r.returncode or not m:
-                return {"error": (r.stdout + r.stderr)[-300:]}
-            ms.append(float(m.group(1)))
+
+    def run(mode):
+        ms = []
+        for _ in range(reps):
+            with tempfile.TemporaryDirectory() as d:
+                os.makedirs(os.path.join(d, "results"))
+                r = subprocess.run([exe, mode], cwd=d, env=env, capture_output=True, text=True, timeout=120)
+                m = re.search(r"closed-loop simulate\s+([0-9.]+) ms", r.stdout + r.stderr)
+                if r.returncode or not m:
+                    return None, (r.stdout + r.stderr)[-300:]
+                ms.append(float(m.group(1)))
+        return ms, None
+
+    ms, err = run("cstr-hempc")
+    if err:
+        return {"error": err}
     med = sorted(ms)[len(ms) // 2]
-    return {"steps": 40, "closed_loop_ms_median": med, "steps_per_s": 40e3 / med, "runs_ms": ms}
+    plain, _ = run("cstr-mpc")  # the same loop with the plaintext regulator (src/ctr.c:406)
+    pmed = sorted(plain)[len(plain) // 2] if plain else None
+    return {"steps": 40, "closed_loop_ms_median": med, "steps_per_s": 40e3 / med, "runs_ms": ms,
+            "plaintext_closed_loop_ms_median": pmed,
+            "encrypted_regulator_ms_per_step": (med - pmed) / 40 if pmed is not None else None}
 
 
 def usable_cpus():

@@ -337,15 +337,17 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
   // row twiddles where they fit) <= 160 KB
   switch (ndig) {
   case 1:
-    ksq_launch<LOGN2, 1, 4, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    // two streams (256 VGPRs); four (1024 threads, 128 VGPRs) spilled 58-193:
+    // 68.2k -> 77.6k ct-mult/s at N=2^16, L=4, dnum=1 (same box)
+    ksq_launch<LOGN2, 1, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
     if (allf)
       ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
-    else
-      ksq_launch<LOGN2, 2, 3, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo,
-                                     t_n);
+    else  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk, 60-bit set)
+      ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+                                           t_lo, t_n);
     break;
   default: gpqhe_die("split key switch: %u digits", ndig);
   }
