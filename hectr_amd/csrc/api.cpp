@@ -405,6 +405,7 @@ extern "C" void hectx_init_params(const gpqhe_params_t *p)
   tables_upload();
   set_seed_words(p->seed ? p->seed : default_seed());
   C.init = true;
+  tables_prewarm();
 }
 
 static unsigned env_u(const char *name, unsigned dflt)
@@ -1103,14 +1104,23 @@ extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const 
 // gain matrices every control step: reference src/hempc.c:232-238).
 // ---------------------------------------------------------------------------
 static std::unordered_map<std::string, uint64_t *> g_gemv_cache;
+static std::vector<void *> g_gemv_blocks;  // what the cache's entries live in (one entry or a batch)
 static size_t g_gemv_cache_bytes = 0;
 
 void gemv_cache_clear()
 {
-  for (auto &kv : g_gemv_cache)
-    pool_free(kv.second);
+  for (void *b : g_gemv_blocks)
+    pool_free(b);
+  g_gemv_blocks.clear();
   g_gemv_cache.clear();
   g_gemv_cache_bytes = 0;
+}
+
+static std::string diag_key(const double *diag, unsigned s, unsigned lvl)
+{
+  std::string key((const char *)diag, (size_t)s * 16);
+  key.append((const char *)&lvl, sizeof(lvl));
+  return key;
 }
 
 // Would encoding one more diagonal at this level overflow the cache (and so
@@ -1123,8 +1133,7 @@ static bool diag_cache_full(unsigned lvl)
 
 static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
 {
-  std::string key((const char *)diag, (size_t)s * 16);
-  key.append((const char *)&lvl, sizeof(lvl));
+  const std::string key = diag_key(diag, s, lvl);
   auto it = g_gemv_cache.find(key);
   if (it != g_gemv_cache.end())
     return it->second;
@@ -1134,6 +1143,7 @@ static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
   if (g_gemv_cache_bytes + bytes > ((size_t)1 << 31))
     gemv_cache_clear();
   uint64_t *p = (uint64_t *)pool_alloc(bytes);
+  g_gemv_blocks.push_back(p);
   encode_limbs(p, diag, s, (double)G.q[lvl - 1], mods, nm);
   g_gemv_cache[key] = p;
   g_gemv_cache_bytes += bytes;
@@ -1265,6 +1275,18 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   }
   PendGemv pg{y->data, pstride(y), limb(x, 0, 0), limb(x, 1, 0), x->data, lvl, {}};
   std::vector<double> diag(2 * (size_t)s);
+  // diagonals not cached yet (host-FFT sizes) are encoded together after the
+  // loop: one upload and one lift + NTT launch for all of them
+  const bool batch_enc = s < gpu_ecd_min();
+  const size_t n = G.n, per = (size_t)(lvl + G.K) << G.logn;
+  std::vector<std::string> newkeys;
+  std::unordered_map<std::string, unsigned> newidx;
+  std::vector<int64_t> newcoef;
+  struct Fix {
+    size_t launch;
+    unsigned e, idx;
+  };
+  std::vector<Fix> fixes;
   // all non-zero diagonals in as few launches as possible (GemvDiags::MAX each)
   GemvDiags dg{};
   for (unsigned d = 0; d < s; d++) {
@@ -1277,7 +1299,27 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     }
     if (!nz)
       continue;
-    const uint64_t *pt = diag_pt(diag.data(), s, lvl);
+    const uint64_t *pt = nullptr;
+    std::string key = diag_key(diag.data(), s, lvl);
+    auto it = g_gemv_cache.find(key);
+    if (it != g_gemv_cache.end()) {
+      pt = it->second;
+    } else if (!batch_enc) {
+      pt = diag_pt(diag.data(), s, lvl);
+    } else {
+      auto jt = newidx.find(key);
+      unsigned idx;
+      if (jt == newidx.end()) {
+        idx = (unsigned)newkeys.size();
+        newidx.emplace(key, idx);
+        newkeys.push_back(std::move(key));
+        newcoef.resize((size_t)(idx + 1) * n);
+        hm_encode_coeffs(newcoef.data() + (size_t)idx * n, diag.data(), s, n, (double)G.q[lvl - 1]);
+      } else {
+        idx = jt->second;
+      }
+      fixes.push_back({pg.dgs.size(), dg.count, idx});
+    }
     const uint64_t g = d == 0 ? 1 : galois_of_rot(d);
     const he_evk_t *k = d == 0 ? nullptr : find_rot_key(rk, d, g);
     dg.evk[dg.count] = k ? k->data : nullptr;
@@ -1290,6 +1332,21 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   }
   if (dg.count)
     pg.dgs.push_back(dg);
+  if (!newkeys.empty()) {
+    const unsigned cnt = (unsigned)newkeys.size();
+    uint64_t *slab = (uint64_t *)pool_alloc((size_t)cnt * per * 8);
+    g_gemv_blocks.push_back(slab);
+    Ws dcoef(newcoef.size());
+    upload(dcoef.p, newcoef.data(), newcoef.size() * 8);
+    unsigned mods[GPQHE_MAXMOD];
+    const unsigned nm = basis_qp(lvl, mods);
+    k_lift_ntt(limbset(slab, mods, nm, cnt, per), (const int64_t *)dcoef.p);
+    for (unsigned i = 0; i < cnt; i++)
+      g_gemv_cache[newkeys[i]] = slab + (size_t)i * per;
+    g_gemv_cache_bytes += (size_t)cnt * per * 8;
+    for (const Fix &f : fixes)
+      pg.dgs[f.launch].pt[f.e] = slab + (size_t)f.idx * per;
+  }
   const double scale = x->scale;
   g_pgemv.push_back(std::move(pg));
   if (!defer)

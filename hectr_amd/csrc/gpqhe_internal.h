@@ -352,4 +352,5 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
 bool k_prof_on();
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
 void tables_upload();
+void tables_prewarm();
 void tables_free();

@@ -1131,7 +1131,7 @@ __global__ void lift_i64_kernel(LimbSet dst, const int64_t *coef, unsigned logn,
     return;
   const unsigned l = blockIdx.y;
   const ModConst c = mc[dst.mod(l)];
-  dst.limb(l, logn)[k] = lift_i64(coef[k], c);
+  dst.limb(l, logn)[k] = lift_i64(coef[((size_t)(l / dst.per) << logn) + k], c);  // one coefficient row per group
 }
 
 void k_lift_i64(const LimbSet &dst, const int64_t *coef)
@@ -3094,6 +3094,23 @@ void tables_upload()
   HIP_CHECK(hipMalloc((void **)&G.itwd, 2 * nm * n * 8));
   HIP_CHECK(hipMemcpy((void *)G.twd, fd.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy((void *)G.itwd, id.data(), 2 * nm * n * 8, hipMemcpyHostToDevice));
+}
+
+// ModUp / ModDown constant tables of every level, built at init rather than
+// at their first use inside a caller's loop (each is a few small uploads).
+void tables_prewarm()
+{
+  for (unsigned lvl = 1; lvl <= G.L; lvl++) {
+    if (G.alpha <= 8)
+      up_table(lvl);
+    if (G.K + 1 <= 8)
+      down_table(lvl, 0);
+    if (lvl >= 2) {
+      if (G.K + 1 <= 8)
+        down_table(lvl, 1);
+      down_table(lvl, 2);
+    }
+  }
 }
 
 void tables_free()
