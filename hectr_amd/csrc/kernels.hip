@@ -2928,11 +2928,10 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
 // ===========================================================================
 static bool split_ndig_ok(unsigned ndig)
 {
-  // the key tile (2 ndig x 16 KB), three padded row tiles (3 x 18 KB) and the
-  // row twiddles (32 KB) fit the LDS for one and two digits; longer keys take
-  // the streaming ks_rows path (config 5, dnum = 3: 7.4k vs 6.8k ct-mult/s
-  // without staged twiddles, same box)
-  return ndig >= 1 && ndig <= 2;
+  // the key tile (2 ndig x 16 KB) + the pair streams' padded row tiles (+ the
+  // staged row twiddles for 1-2 digits) fit the LDS up to three digits;
+  // longer keys take the streaming ks_rows path
+  return ndig >= 1 && ndig <= 3;
 }
 
 bool k_mul_split_ok(unsigned lvl)

@@ -349,6 +349,17 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
       ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
                                            t_lo, t_n);
     break;
+  case 3:
+    // 96 KB of key tile: two streams and the row twiddles from L2 (config 5:
+    // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
+    // staged twiddles 7.50k, same box)
+    if (allf)
+      ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+                                           t_lo, t_n);
+    else
+      ksq_launch<LOGN2, 3, 2, false, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+                                            t_lo, t_n);
+    break;
   default: gpqhe_die("split key switch: %u digits", ndig);
   }
 }
