@@ -13,7 +13,7 @@ if [ -z "$NO_TESTS" ]; then
     --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log; [ $rc -eq 0 ] || exit 1
 fi
-B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr --no-ntt --alt-bits 0 ${BENCH_ARGS}"
+B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr ${LEGS:---no-ntt} --alt-bits 0 ${BENCH_ARGS}"
 for r in $(seq 1 ${ROUNDS:-2}); do
   GPQHE_LIB=hectr_amd/lib_base/libgpqhe.so timeout -k 10 300 $B > $OUT/bench_base_$r.log 2>&1 || exit 1
   timeout -k 10 300 $B > $OUT/bench_new_$r.log 2>&1 || exit 1
