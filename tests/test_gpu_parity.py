@@ -296,6 +296,41 @@ def test_gemv_zero_matrix(oracle, product):
     assert np.abs(e.decrypt(y, sk)).max() < 1e-6
 
 
+@pytest.mark.parametrize("name", ["ref", "c1", "hyb"])
+def test_gemv_queue(oracle, product, name):
+    """Queued he_gemv calls (api.cpp:flush_gemvs): two independent gemvs run as
+    one batch (one ModUp over both inputs, one inner-product launch, one
+    ModDown with two outputs: the fused small-N kernels at n=4096, the
+    down_combine two-output split at n=2^13); a third that reads the second's
+    output and an all-zero matrix queued beside a non-zero one.  Every output
+    bit-exact with the oracle's sequential calls."""
+    init_both(oracle, product, name)
+    rng = np.random.default_rng(17)
+    s = oracle.slots
+    z1 = rng.uniform(-1, 1, s) + 0j
+    z2 = rng.uniform(-1, 1, s) + 0j
+    M1, M2, M3 = (rng.uniform(-2, 2, (s, s)) for _ in range(3))
+    Z = np.zeros((s, s))
+    res = {}
+    for e in (oracle, product):
+        pk, sk, rk, _ = keys(e)
+        a, b = e.encrypt(z1, pk), e.encrypt(z2, pk)
+        y1, y2, y3, y4, y5 = (e.ct() for _ in range(5))
+        e.gemv(y1, M1.ravel(), a, rk)
+        e.gemv(y2, M2.ravel(), b, rk)  # independent: batched with y1
+        chain = e.L >= 3  # y2 is one level down; HECTR's own L = 2 has no room for a second gemv
+        e.gemv(y3, M3.ravel(), y2 if chain else a, rk)  # reads y2: runs after the batch
+        e.gemv(y4, Z.ravel(), a, rk)  # all-zero matrix queued beside y5
+        e.gemv(y5, M1.ravel(), b, rk)
+        res[e.name] = ([y1, y2, y3, y4, y5], sk)
+    for o, p in zip(res["oracle"][0], res["product"][0]):
+        same(oracle, product, o, p)
+    ys, sk = res["product"]
+    want = [M1 @ z1, M2 @ z2, M3 @ (M2 @ z2) if product.L >= 3 else M3 @ z1, 0 * z1, M1 @ z2]
+    for y, w in zip(ys, want):
+        assert np.abs(product.decrypt(y, sk) - w).max() < 1e-5 * max(1.0, np.abs(w).max())
+
+
 
 @pytest.mark.parametrize("name,slots", [("c1", 2048), ("c1", 4096), ("bench51", 32768), ("bench51", 4096)])
 def test_gpu_encode_bitexact(oracle, product, name, slots):
