@@ -216,7 +216,8 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
 
 
 @pytest.mark.parametrize("name,cnt,chunk", [("bench51", 17, None), ("bench51", 24, None), ("bench_d2", 17, None),
-                                            ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None)])
+                                            ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None),
+                                            ("c5", 17, None), ("c15", 17, None)])
 def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
     """The headline shape (bench.py): n=2^16, L=8,
     dnum=2, K=4 on 17 and 24 pairs (the split key switch's pair ranges of
@@ -225,7 +226,9 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     the accumulator restart), 17 pairs in chunks of 5/5/5/2 (the multi-chunk
     loop, a short last chunk) and the bench's own 256 pairs (two 128-pair
     chunks of the 8 GiB workspace, about 3 pairs per quarter), every output
-    residue compared with the oracle."""
+    residue compared with the oracle.  Also 17 pairs of config 5 (n=2^17, L=12,
+    the three-digit split key switch) and of c15 (integer moduli: two pair
+    streams per workgroup)."""
     if chunk:
         monkeypatch.setenv("GPQHE_CHUNK", str(chunk))
     want, got = mul_batch_both(oracle, product, name, cnt, seeds=(21, 22))
