@@ -797,10 +797,11 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     k_ntt_ex(qlimbs(pt->data, nl, 1, words), qlimbs(c.p, nl, 1, words), true, nullptr);
     src = c.p;
   }
-  std::vector<uint64_t> host(words);
-  HIP_CHECK(hipMemcpyAsync(host.data(), src, words * 8, hipMemcpyDeviceToHost, G.stream));
+  // CRT lift + FFT on the GPU (k_decode); only the s values cross PCIe
+  Ws zd(2 * (size_t)slots);
+  k_decode((double *)zd.p, src, nl, slots, pt->scale);
+  HIP_CHECK(hipMemcpyAsync(z, zd.p, (size_t)slots * 16, hipMemcpyDeviceToHost, G.stream));
   HIP_CHECK(hipStreamSynchronize(G.stream));
-  hm_decode((double *)z, host.data(), nl, slots, G.n, pt->scale);
 }
 
 extern "C" void he_dcd(gpqhe_complex_t z[], const he_pt_t *pt)

@@ -233,8 +233,10 @@ void hm_fft_tables(unsigned s, double *ksi, unsigned *rot);
 // operations, same order: bit-identical).  Synchronises (overflow check).
 void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale);
 void hm_encode_coeffs(int64_t *coef, const double *z_interleaved, unsigned s, unsigned n, double scale);
-void hm_decode(double *z_interleaved, const uint64_t *coef_limbs, unsigned nl, unsigned s, unsigned n,
-               double scale);
+// GPU decoder: z (device, s complex values) <- the centred CRT lift of the
+// coefficient limbs coef [nl][n] (device), / scale, forward special FFT --
+// bit-identical to the oracle's he_dcd; asynchronous on the engine stream.
+void k_decode(double *z, const uint64_t *coef, unsigned nl, unsigned s, double scale);
 
 // ---------------------------------------------------------------------------
 // Device memory pool (stream-ordered reuse on the engine stream).

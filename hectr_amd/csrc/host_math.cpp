@@ -4,7 +4,8 @@
 // those already chosen; psi = h^((q-1)/2n) for the smallest h >= 2 with
 // psi^n = -1.  Encode: inverse special FFT over the 4s-th roots with
 // rotation group 5^j, coefficients at stride n/(2s), llround(value * scale).
-// Decode: centred CRT lift (Garner), / scale, forward special FFT.
+// Decode (centred CRT lift, / scale, forward special FFT) runs on the GPU:
+// kernels.hip k_decode.
 // These are the definitions of oracle/ckks_oracle.c; the complex arithmetic
 // is spelled out in real operations and built with -ffp-contract=off so the
 // doubles round identically.
@@ -190,23 +191,6 @@ static void bitrev_perm(cplx *v, unsigned s)
   }
 }
 
-static void fft_special_dec(cplx *v, unsigned s)
-{
-  FftTables T(s);
-  const unsigned M = 4 * s;
-  bitrev_perm(v, s);
-  for (unsigned len = 2; len <= s; len <<= 1) {
-    const unsigned h = len >> 1, lq = len << 2;
-    for (unsigned i = 0; i < s; i += len)
-      for (unsigned j = 0; j < h; j++) {
-        const unsigned idx = (T.rot[j] % lq) * (M / lq);
-        const cplx a = v[i + j], b = cmul(v[i + j + h], T.ksi[idx]);
-        v[i + j] = {a.re + b.re, a.im + b.im};
-        v[i + j + h] = {a.re - b.re, a.im - b.im};
-      }
-  }
-}
-
 static void fft_special_enc(cplx *v, unsigned s)
 {
   FftTables T(s);
@@ -244,95 +228,5 @@ void hm_encode_coeffs(int64_t *coef, const double *z, unsigned s, unsigned n, do
       gpqhe_die("encode overflow (|value * scale| >= 2^63)");
     coef[(size_t)k * gap] = llround(re);
     coef[(size_t)(k + s) * gap] = llround(im);
-  }
-}
-
-// Centred CRT lift of residues over q_0..q_{nl-1} (Garner), as double.
-static double crt_center(const uint64_t *res, unsigned nl)
-{
-  if (nl == 1) {
-    const uint64_t v = res[0], q = G.q[0];
-    return v > q / 2 ? -(double)(q - v) : (double)v;
-  }
-  uint64_t v[GPQHE_MAXMOD];
-  for (unsigned i = 0; i < nl; i++) {
-    const uint64_t qi = G.q[i];
-    uint64_t t = res[i];
-    for (unsigned j = 0; j < i; j++) {
-      const uint64_t vj = v[j] % qi;
-      t = t >= vj ? t - vj : t + qi - vj;
-      t = hm_mul_mod(t, hm_inv_mod(G.q[j] % qi, qi), qi);
-    }
-    v[i] = t;
-  }
-  uint64_t val[GPQHE_MAXMOD + 1], Q[GPQHE_MAXMOD + 1];
-  memset(val, 0, sizeof(val));
-  memset(Q, 0, sizeof(Q));
-  val[0] = v[nl - 1];
-  Q[0] = 1;
-  for (int i = (int)nl - 2; i >= 0; i--) {
-    u128 carry = v[i];
-    for (unsigned w = 0; w <= nl; w++) {
-      const u128 x = (u128)val[w] * G.q[i] + carry;
-      val[w] = (uint64_t)x;
-      carry = x >> 64;
-    }
-  }
-  for (unsigned i = 0; i < nl; i++) {
-    u128 carry = 0;
-    for (unsigned w = 0; w <= nl; w++) {
-      const u128 x = (u128)Q[w] * G.q[i] + carry;
-      Q[w] = (uint64_t)x;
-      carry = x >> 64;
-    }
-  }
-  bool neg = false;
-  {
-    uint64_t twice[GPQHE_MAXMOD + 1];
-    uint64_t c = 0;
-    for (unsigned w = 0; w <= nl; w++) {
-      twice[w] = (val[w] << 1) | c;
-      c = val[w] >> 63;
-    }
-    for (int w = (int)nl; w >= 0; w--)
-      if (twice[w] != Q[w]) {
-        neg = twice[w] > Q[w];
-        break;
-      }
-  }
-  if (neg) {
-    uint64_t b = 0;
-    for (unsigned w = 0; w <= nl; w++) {
-      const u128 x = (u128)Q[w] - val[w] - b;
-      val[w] = (uint64_t)x;
-      b = (uint64_t)(x >> 64) & 1;
-    }
-  }
-  double d = 0;
-  for (int w = (int)nl; w >= 0; w--)
-    d = d * 18446744073709551616.0 + (double)val[w];
-  return neg ? -d : d;
-}
-
-void hm_decode(double *z, const uint64_t *c, unsigned nl, unsigned s, unsigned n, double scale)
-{
-  if (!s || (s & (s - 1)) || s > n / 2)
-    gpqhe_die("bad slot count %u", s);
-  const unsigned gap = n / (2 * s);
-  std::vector<cplx> u(s);
-  uint64_t res[GPQHE_MAXMOD];
-  for (unsigned k = 0; k < s; k++) {
-    for (unsigned m = 0; m < nl; m++)
-      res[m] = c[(size_t)m * n + (size_t)k * gap];
-    const double re = crt_center(res, nl);
-    for (unsigned m = 0; m < nl; m++)
-      res[m] = c[(size_t)m * n + (size_t)(k + s) * gap];
-    const double im = crt_center(res, nl);
-    u[k] = {re / scale, im / scale};
-  }
-  fft_special_dec(u.data(), s);
-  for (unsigned i = 0; i < s; i++) {
-    z[2 * i] = u[i].re;
-    z[2 * i + 1] = u[i].im;
   }
 }

@@ -1079,10 +1079,9 @@ struct FftDev {
 };
 static std::map<unsigned, FftDev> g_fft;
 
-void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale)
+static const FftDev &fft_dev(unsigned s)
 {
-  const unsigned n = G.n;
-  if (!s || (s & (s - 1)) || s > n / 2)
+  if (!s || (s & (s - 1)) || s > G.n / 2)
     gpqhe_die("bad slot count %u", s);
   auto it = g_fft.find(s);
   if (it == g_fft.end()) {
@@ -1096,7 +1095,13 @@ void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale)
     HIP_CHECK(hipMemcpy(d.rot, rot.data(), rot.size() * 4, hipMemcpyHostToDevice));
     it = g_fft.emplace(s, d).first;
   }
-  const FftDev &T = it->second;
+  return it->second;
+}
+
+void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale)
+{
+  const unsigned n = G.n;
+  const FftDev &T = fft_dev(s);
   double2 *v = (double2 *)work;
   unsigned len = s;
   for (; len > FFT_LDS; len >>= 1)
@@ -1117,6 +1122,187 @@ void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale)
     gpqhe_die("encode overflow (|value * scale| >= 2^63)");
 }
 
+// ---------------------------------------------------------------------------
+// GPU CKKS decoder (he_dcd): the centred CRT lift (Garner) of the 2s
+// coefficients the slots read, / scale, and the special forward FFT of
+// host_math.cpp (hm_decode: crt_center, fft_special_dec) with the same
+// integer steps and the same IEEE operations in the same order (no
+// contraction), so bit-identical to the host decoder and the oracle
+// (oracle/ckks_oracle.c crt_center / he_dcd_ex).  Only the s decoded values
+// cross PCIe instead of nl limbs of n residues.
+//   fft_dec_lds_kernel: a block per FFT_LDS-element chunk of the bit-reversed
+//     vector lifts its elements straight into LDS and runs the stages
+//     len = 2 .. chunk there;
+//   fft_dec_stage_kernel: the stages with len > FFT_LDS, a thread per butterfly.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fft_dec_bfly(double2 &x, double2 &y, const double2 w)
+{
+  const double2 a = x;
+  const double2 b = make_double2(y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x);
+  x = make_double2(a.x + b.x, a.y + b.y);
+  y = make_double2(a.x - b.x, a.y - b.y);
+}
+
+// Centred lift of coefficient k over q_0..q_{nl-1} (nl <= NLM), as double.
+// ginv[i * ld + j] = (q_j mod q_i)^-1 mod q_i.  Words above nl stay zero, so
+// the fixed-length loops give the host's values exactly.
+template <int NLM>
+__device__ double dcd_crt_center(const uint64_t *c, unsigned k, unsigned nl, unsigned logn, const ModConst *mc,
+                                 const uint64_t *ginv, unsigned ld)
+{
+  constexpr int U = NLM <= 16 ? NLM + 1 : 1;  // registers up to 16 limbs
+  if (nl == 1) {
+    const uint64_t v = c[k], q = mc[0].q;
+    return v > q / 2 ? -(double)(q - v) : (double)v;
+  }
+  uint64_t v[NLM];
+#pragma unroll U
+  for (int i = 0; i < NLM; i++) {
+    v[i] = 0;
+    if (i < (int)nl) {
+      const ModConst m = mc[i];
+      uint64_t t = c[((size_t)i << logn) + k];
+#pragma unroll U
+      for (int j = 0; j < i; j++) {
+        t = sub_mod(t, reduce64(v[j], m), m.q);
+        t = mul_mod(t, ginv[i * ld + j], m);
+      }
+      v[i] = t;
+    }
+  }
+  // val = v_{nl-1}; val = val q_i + v_i for i = nl-2 .. 0 (Horner from 0);
+  // Q = prod q_i
+  uint64_t val[NLM + 1], Q[NLM + 1];
+#pragma unroll U
+  for (int w = 0; w <= NLM; w++)
+    val[w] = Q[w] = 0;
+  Q[0] = 1;
+#pragma unroll U
+  for (int i = NLM - 1; i >= 0; i--) {
+    if (i < (int)nl) {
+      const uint64_t q = mc[i].q;
+      uint64_t cv = v[i], cq = 0;
+#pragma unroll U
+      for (int w = 0; w <= NLM; w++) {
+        uint64_t lo = val[w] * q, hi = __umul64hi(val[w], q);
+        lo += cv;
+        hi += lo < cv;
+        val[w] = lo;
+        cv = hi;
+        uint64_t ql = Q[w] * q, qh = __umul64hi(Q[w], q);
+        ql += cq;
+        qh += ql < cq;
+        Q[w] = ql;
+        cq = qh;
+      }
+    }
+  }
+  // negative iff 2 val > Q
+  int cmp = 0;
+  uint64_t carry = 0;
+  uint64_t twice[NLM + 1];
+#pragma unroll U
+  for (int w = 0; w <= NLM; w++) {
+    twice[w] = (val[w] << 1) | carry;
+    carry = val[w] >> 63;
+  }
+#pragma unroll U
+  for (int w = NLM; w >= 0; w--)
+    if (!cmp && twice[w] != Q[w])
+      cmp = twice[w] > Q[w] ? 1 : -1;
+  const bool neg = cmp > 0;
+  if (neg) {
+    uint64_t b = 0;
+#pragma unroll U
+    for (int w = 0; w <= NLM; w++) {
+      const uint64_t d = Q[w] - val[w], d2 = d - b;
+      b = (Q[w] < val[w]) | (d < b);
+      val[w] = d2;
+    }
+  }
+  double d = 0;
+#pragma unroll U
+  for (int w = NLM; w >= 0; w--)
+    d = d * 18446744073709551616.0 + (double)val[w];
+  return neg ? -d : d;
+}
+
+template <int NLM>
+__global__ void __launch_bounds__(512) fft_dec_lds_kernel(double2 *v, const uint64_t *c, unsigned nl, unsigned logn,
+                                                          unsigned s, unsigned logs, unsigned len0, double scale,
+                                                          const ModConst *mc, const uint64_t *ginv, unsigned ld,
+                                                          const double2 *ksi, const unsigned *rot)
+{
+  __shared__ double2 sh[FFT_LDS];
+  const unsigned base = blockIdx.x * len0, M = 4 * s, gap = (1u << logn) / (2 * s);
+  for (unsigned e = threadIdx.x; e < len0; e += blockDim.x) {
+    const unsigned slot = logs ? __brev(base + e) >> (32 - logs) : 0;  // v = bit-reversed u
+    const double re = dcd_crt_center<NLM>(c, slot * gap, nl, logn, mc, ginv, ld);
+    const double im = dcd_crt_center<NLM>(c, (slot + s) * gap, nl, logn, mc, ginv, ld);
+    sh[e] = make_double2(re / scale, im / scale);
+  }
+  __syncthreads();
+  for (unsigned len = 2; len <= len0; len <<= 1) {
+    const unsigned h = len >> 1, lq = len << 2;
+    for (unsigned t = threadIdx.x; t < len0 / 2; t += blockDim.x) {
+      const unsigned i = (t / h) * len, j = t % h;
+      fft_dec_bfly(sh[i + j], sh[i + j + h], ksi[(rot[j] % lq) * (M / lq)]);
+    }
+    __syncthreads();
+  }
+  for (unsigned e = threadIdx.x; e < len0; e += blockDim.x)
+    v[base + e] = sh[e];
+}
+
+__global__ void fft_dec_stage_kernel(double2 *v, unsigned s, unsigned len, const double2 *ksi, const unsigned *rot)
+{
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= s / 2)
+    return;
+  const unsigned h = len >> 1, lq = len << 2, M = 4 * s;
+  const unsigned i = (t / h) * len, j = t % h;
+  fft_dec_bfly(v[i + j], v[i + j + h], ksi[(rot[j] % lq) * (M / lq)]);
+}
+
+static uint64_t *g_ginv = nullptr;  // [L][L] Garner inverses of the current context
+
+void k_decode(double *z, const uint64_t *coef, unsigned nl, unsigned s, double scale)
+{
+  const FftDev &T = fft_dev(s);
+  if (nl < 1 || nl > G.L)
+    gpqhe_die("he_dcd: bad level %u", nl);
+  const unsigned ld = G.L;
+  if (!g_ginv) {
+    std::vector<uint64_t> h((size_t)ld * ld, 0);
+    for (unsigned i = 0; i < ld; i++)
+      for (unsigned j = 0; j < i; j++)
+        h[(size_t)i * ld + j] = hm_inv_mod(G.q[j] % G.q[i], G.q[i]);
+    HIP_CHECK(hipMalloc(&g_ginv, h.size() * 8));
+    HIP_CHECK(hipMemcpy(g_ginv, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  }
+  double2 *v = (double2 *)z;
+  const unsigned logs = (unsigned)__builtin_ctz(s), len0 = std::min(s, FFT_LDS);
+  const dim3 grid(s / len0), block(std::min(512u, std::max(64u, len0 / 2)));
+#define GPQHE_DCD(NLM)                                                                                     \
+  hipLaunchKernelGGL(fft_dec_lds_kernel<NLM>, grid, block, 0, G.stream, v, coef, nl, G.logn, s, logs, len0, \
+                     scale, G.dev.mc, g_ginv, ld, T.ksi, T.rot)
+  if (nl <= 2)
+    GPQHE_DCD(2);
+  else if (nl <= 4)
+    GPQHE_DCD(4);
+  else if (nl <= 8)
+    GPQHE_DCD(8);
+  else if (nl <= 16)
+    GPQHE_DCD(16);
+  else
+    GPQHE_DCD(GPQHE_MAXMOD);
+#undef GPQHE_DCD
+  for (unsigned len = 2 * len0; len <= s; len <<= 1)
+    hipLaunchKernelGGL(fft_dec_stage_kernel, dim3((s / 2 + TPB - 1) / TPB), dim3(TPB), 0, G.stream, v, s, len,
+                       T.ksi, T.rot);
+  HIP_CHECK(hipGetLastError());
+}
+
 void k_fft_free()
 {
   for (auto &kv : g_fft) {
@@ -1124,6 +1310,9 @@ void k_fft_free()
     HIP_CHECK(hipFree(kv.second.rot));
   }
   g_fft.clear();
+  if (g_ginv)
+    HIP_CHECK(hipFree(g_ginv));
+  g_ginv = nullptr;
 }
 
 __global__ void lift_i64_kernel(LimbSet dst, const int64_t *coef, unsigned logn, const ModConst *mc)

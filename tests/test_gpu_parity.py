@@ -362,3 +362,34 @@ def test_gpu_encode_bitexact(oracle, product, name, slots):
     assert np.abs(got - z).max() < 1e-6
     for o in (pt, ct, dec):
         product.free(o)
+
+
+@pytest.mark.parametrize("name,slots,nl", [("ref", 16, 2), ("ref", 2048, 1), ("c1", 64, 3), ("c1", 4096, 4),
+                                           ("bench51", 32768, 8), ("c5", 8192, 12)])
+def test_gpu_decode_bitexact(oracle, product, name, slots, nl):
+    """he_dcd on the GPU (kernels.hip k_decode: centred CRT lift + special
+    forward FFT) against the oracle's host decode, bit for bit.  Uniform random
+    residues decode to full-width values of both signs (|x| up to Q/2, every
+    word of the multi-word lift); both the NTT-form input (inverse transform
+    first) and a coefficient-form one (GPQHE_F_COEFF).  Slot counts cover one
+    LDS chunk (16..2048) and the global stages above 2048; nl = 1 (the
+    single-limb shortcut) up to 12 limbs."""
+    init_both(oracle, product, name)
+    n = product.n
+    rng = np.random.default_rng(slots + nl)
+    res = np.stack([rng.integers(0, q, n, dtype=np.uint64) for q in product.primes[:nl]])
+    # small centred values on a second plaintext: the decrypt-range branch
+    small = rng.integers(-2 ** 40, 2 ** 40, n)
+    res_small = np.stack([(small % q).astype(np.uint64) for q in product.primes[:nl]])
+    scale = 2.0 ** 40
+    for arr in (res, res_small):
+        for flags in (0, 1):
+            got = {}
+            for e in (oracle, product):
+                pt = e.pt()
+                e.import_(pt, arr, nl, scale, flags)
+                got[e.name] = e.dcd(pt, slots)
+                e.free(pt)
+            o, p = got["oracle"], got["product"]
+            assert np.array_equal(o.view(np.uint64), p.view(np.uint64)), \
+                f"{np.count_nonzero(o != p)} of {slots} decoded slots differ (flags={flags})"
