@@ -27,6 +27,8 @@ static size_t pool_round(size_t b)
   return (b + 4095) & ~(size_t)4095;
 }
 
+static void flush_ew();
+
 void *pool_alloc(size_t bytes)
 {
   const size_t b = pool_round(bytes ? bytes : 1);
@@ -39,7 +41,9 @@ void *pool_alloc(size_t bytes)
   void *p = nullptr;
   hipError_t e = hipMalloc(&p, b);
   if (e != hipSuccess) {
-    // give cached blocks back and retry once
+    // give cached blocks back and retry once (queued elementwise ops may
+    // still name a free-listed block: they run first)
+    flush_ew();
     HIP_CHECK(hipStreamSynchronize(G.stream));
     for (auto &kv : g_free)
       for (void *q : kv.second) {
@@ -163,13 +167,32 @@ struct PendGemv {
 };
 static std::vector<PendGemv> g_pgemv;
 
+// The elementwise calls of a control step (he_sub x2 before the gemvs; he_add,
+// he_neg, he_copy_ct, he_add after them, src/hempc.c:253-266; he_dec,
+// src/ctr.c:486) are queued too and run as one ew_prog_kernel launch per run
+// (kernels.hip).  The queue keeps call order element by element, so a freed
+// object's block may be handed out again while queued ops still name it:
+// every writer outside this queue flushes it first.  The three queues are
+// never non-empty at once.
+static EwProg g_pew{};
+
 static void flush_pending();
 static void flush_gemvs();
+
+static void flush_ew()
+{
+  if (!g_pew.count)
+    return;
+  const EwProg p = g_pew;
+  g_pew.count = 0;
+  k_ew_prog(p);
+}
 
 static void check_ctx()
 {
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
+  flush_ew();
   if (!g_pgemv.empty())
     flush_gemvs();
   if (!g_pecd.empty() || !g_penc.empty())
@@ -237,8 +260,10 @@ static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
 
 static void obj_free(void *vo)
 {
-  if (G.init)
-    check_ctx();  // a queued encode / encryption may still use the payload
+  // a queued encode / encryption / gemv may still use the payload (queued
+  // elementwise ops keep their order with any later user of the block)
+  if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty()))
+    check_ctx();
   he_ct_t *o = OB(vo);
   if (o->data && G.init)
     pool_free(o->data);
@@ -756,6 +781,7 @@ extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int s
   if (defer_ok(slots)) {
     // queued (flush_pending); a plaintext a queued encryption still reads, or
     // a queued encode target, is flushed first
+    flush_ew();
     if (!g_pgemv.empty())
       flush_gemvs();
     bool busy = false;
@@ -816,6 +842,7 @@ extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
   const unsigned lvl = pt->nlimbs;
   if (defer_ok(0)) {
     // queued (flush_pending): streams taken now, in call order
+    flush_ew();
     if (!g_pgemv.empty())
       flush_gemvs();
     bool busy = false;
@@ -871,8 +898,37 @@ extern "C" void he_enc_sk(he_ct_t *ct, const he_pt_t *pt, const poly_mpi_t *sk)
   ct->flags = 0;
 }
 
+// Queue elementwise ops (defer_ok(0): n <= 2^12); false: run them now.
+static bool ew_defer(unsigned nops)
+{
+  if (!defer_ok(0))
+    return false;
+  if (!g_pgemv.empty())
+    flush_gemvs();
+  if (!g_pecd.empty() || !g_penc.empty())
+    flush_pending();
+  if (g_pew.count + nops > EwProg::MAX)
+    flush_ew();
+  return true;
+}
+
+static void ew_push(uint32_t kind, uint64_t *out, const uint64_t *a, const uint64_t *b, const uint64_t *sk,
+                    unsigned lvl)
+{
+  g_pew.op[g_pew.count++] = EwOp{out, a, b, sk, kind, lvl};
+}
+
 extern "C" void he_dec(he_pt_t *pt, const he_ct_t *ct, const poly_mpi_t *sk)
 {
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
+  if (ew_defer(1)) {
+    ew_push(EW_DEC, pt->data, limb(ct, 0, 0), limb(ct, 1, 0), sk->data, ct->nlimbs);
+    pt->nlimbs = ct->nlimbs;
+    pt->scale = ct->scale;
+    pt->flags = 0;
+    return;
+  }
   check_ctx();
   k_dec(pt->data, limb(ct, 0, 0), limb(ct, 1, 0), sk->data, ct->nlimbs);
   pt->nlimbs = ct->nlimbs;
@@ -891,11 +947,18 @@ static void check_scales(double a, double b, const char *op)
 
 static void addsub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, int op)
 {
-  check_ctx();
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
   check_scales(a->scale, b->scale, op ? "he_sub" : "he_add");
   const unsigned lvl = std::min(a->nlimbs, b->nlimbs);
   const double scale = a->scale;
-  k_binop(out->data, a->data, b->data, 2, lvl, pstride(out), pstride(a), pstride(b), op);
+  if (ew_defer(2)) {
+    for (unsigned p = 0; p < 2; p++)
+      ew_push(op ? EW_SUB : EW_ADD, limb(out, p, 0), limb(a, p, 0), limb(b, p, 0), nullptr, lvl);
+  } else {
+    check_ctx();
+    k_binop(out->data, a->data, b->data, 2, lvl, pstride(out), pstride(a), pstride(b), op);
+  }
   out->nlimbs = lvl;
   out->scale = scale;
   out->flags = 0;
@@ -906,18 +969,32 @@ extern "C" void he_sub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b) { addsu
 
 extern "C" void he_neg(he_ct_t *ct)
 {
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
+  if (ew_defer(2)) {
+    for (unsigned p = 0; p < 2; p++)
+      ew_push(EW_NEG, limb(ct, p, 0), limb(ct, p, 0), nullptr, nullptr, ct->nlimbs);
+    return;
+  }
   check_ctx();
   k_neg(ct->data, 2, ct->nlimbs, pstride(ct));
 }
 
 extern "C" void he_copy_ct(he_ct_t *dst, const he_ct_t *src)
 {
-  check_ctx();
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
   if (dst == src)
     return;
-  const size_t bytes = ((size_t)src->nlimbs << G.logn) * 8;
-  for (unsigned p = 0; p < 2; p++)
-    HIP_CHECK(hipMemcpyAsync(limb(dst, p, 0), limb(src, p, 0), bytes, hipMemcpyDeviceToDevice, G.stream));
+  if (ew_defer(2)) {
+    for (unsigned p = 0; p < 2; p++)
+      ew_push(EW_COPY, limb(dst, p, 0), limb(src, p, 0), nullptr, nullptr, src->nlimbs);
+  } else {
+    check_ctx();
+    const size_t bytes = ((size_t)src->nlimbs << G.logn) * 8;
+    for (unsigned p = 0; p < 2; p++)
+      HIP_CHECK(hipMemcpyAsync(limb(dst, p, 0), limb(src, p, 0), bytes, hipMemcpyDeviceToDevice, G.stream));
+  }
   dst->nlimbs = src->nlimbs;
   dst->scale = src->scale;
   dst->flags = src->flags;
@@ -925,7 +1002,9 @@ extern "C" void he_copy_ct(he_ct_t *dst, const he_ct_t *src)
 
 extern "C" void he_moddown(he_ct_t *ct)
 {
-  check_ctx();
+  // bookkeeping only (queued work captured its levels): no flush
+  if (!G.init)
+    gpqhe_die("context not initialised (hectx_init)");
   if (ct->nlimbs < 2)
     gpqhe_die("he_moddown: ciphertext at the lowest level");
   ct->nlimbs--;
@@ -937,8 +1016,10 @@ extern "C" void he_add_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt)
   check_scales(a->scale, pt->scale, "he_add_pt");
   const unsigned lvl = std::min(a->nlimbs, pt->nlimbs);
   const double scale = a->scale;
-  if (out != a)
+  if (out != a) {
     he_copy_ct(out, a);
+    flush_ew();  // the copy may have been queued
+  }
   k_add_pt(out->data, out->data, pt->data, lvl, pstride(out));
   out->nlimbs = lvl;
   out->scale = scale;
@@ -1250,6 +1331,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
 {
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
+  flush_ew();  // x may be a queued difference
   if (!g_pecd.empty() || !g_penc.empty())
     flush_pending();  // x may be a queued encryption
   const unsigned lvl = x->nlimbs, s = G.slots;

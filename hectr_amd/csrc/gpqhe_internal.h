@@ -259,6 +259,22 @@ void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t pstride);
 void k_tensor(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b, unsigned lvl,
               size_t in_stride, size_t in_pstride, unsigned count, size_t d_stride);
 void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned lvl);
+// Deferred elementwise program (the small-N latency path, api.cpp): queued
+// he_add / he_sub / he_neg / he_copy_ct / he_dec polys, applied in queue order
+// to every element (limb, k) by one launch.  Op: out = a + b, a - b, -a, a, or
+// a + b s (decryption: a = c0, b = c1, s = the secret key), limbs < lvl.
+enum { EW_ADD = 0, EW_SUB = 1, EW_NEG = 2, EW_COPY = 3, EW_DEC = 4 };
+struct EwOp {
+  uint64_t *out;
+  const uint64_t *a, *b, *s;
+  uint32_t kind, lvl;
+};
+struct EwProg {
+  static constexpr unsigned MAX = 16;
+  EwOp op[MAX];
+  unsigned count;
+};
+void k_ew_prog(const EwProg &p);
 void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);

@@ -910,6 +910,56 @@ void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t 
   HIP_CHECK(hipGetLastError());
 }
 
+// One launch for a queued elementwise program: thread (limb, k) applies the
+// ops in queue order to its element.  Each op reads and writes only element
+// (limb, k) of its operands, so every value is the one of the sequential
+// binop / neg / copy / dec launches.
+__global__ void ew_prog_kernel(EwProg pr, unsigned logn, const ModConst *mc)
+{
+  const size_t n = (size_t)1 << logn;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  const unsigned l = blockIdx.y;
+  const ModConst m = mc[l];
+  const size_t off = ((size_t)l << logn) + i;
+  for (unsigned j = 0; j < pr.count; j++) {
+    const EwOp &o = pr.op[j];
+    if (l >= o.lvl)
+      continue;
+    const uint64_t x = o.a[off];
+    uint64_t r;
+    switch (o.kind) {
+    case EW_ADD:
+      r = add_mod(x, o.b[off], m.q);
+      break;
+    case EW_SUB:
+      r = sub_mod(x, o.b[off], m.q);
+      break;
+    case EW_NEG:
+      r = neg_mod(x, m.q);
+      break;
+    case EW_DEC:
+      r = add_mod(x, mul_mod(o.b[off], o.s[off], m), m.q);
+      break;
+    default:
+      r = x;
+    }
+    o.out[off] = r;
+  }
+}
+
+void k_ew_prog(const EwProg &p)
+{
+  unsigned lv = 0;
+  for (unsigned j = 0; j < p.count; j++)
+    lv = std::max(lv, p.op[j].lvl);
+  if (!lv)
+    return;
+  hipLaunchKernelGGL(ew_prog_kernel, dim3((G.n + TPB - 1) / TPB, lv), dim3(TPB), 0, G.stream, p, G.logn, G.dev.mc);
+  HIP_CHECK(hipGetLastError());
+}
+
 // Small samples (ternary or CBD-21) lifted to every limb of dst.
 __global__ void sample_small_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, int cbd,
                                     const ModConst *mc)

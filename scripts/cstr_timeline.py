@@ -23,7 +23,11 @@ for r in load("*kernel_trace.csv"):
 for r in load("*memory_copy_trace.csv"):
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", r.get("Direction", r.get("Operation", "copy"))))
 ev.sort()
+print("files:", [os.path.relpath(f, d) for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True)])
+print("copy kinds:", sorted({e[3] for e in ev if e[2] == "C"}))
 ends = [i for i, e in enumerate(ev) if e[2] == "C" and "DEVICE_TO_HOST" in e[3].upper()]
+if len(ends) < 4:  # no copy trace: the decoder's last kernel ends each step
+    ends = [i for i, e in enumerate(ev) if e[2] == "K" and e[3].startswith("void fft_dec")]
 steps = []
 for a, b in zip(ends[:-1], ends[1:]):
     seg = ev[a + 1:b + 1]

@@ -393,3 +393,43 @@ def test_gpu_decode_bitexact(oracle, product, name, slots, nl):
             o, p = got["oracle"], got["product"]
             assert np.array_equal(o.view(np.uint64), p.view(np.uint64)), \
                 f"{np.count_nonzero(o != p)} of {slots} decoded slots differ (flags={flags})"
+
+
+@pytest.mark.parametrize("name", ["ref", "c1"])
+def test_ew_queue_sequences(oracle, product, name):
+    """The queued elementwise calls at n <= 2^12 (api.cpp g_pew: he_add /
+    he_sub / he_neg / he_copy_ct / he_dec as one ew_prog_kernel launch) keep
+    call order: aliasing outputs, a level drop (he_moddown) between queued
+    ops, a freed object whose block is handed out again while queued ops
+    still name it (next user queued, and next user an unqueued he_mul), and a
+    decryption queued behind them -- bit-exact vs the oracle's sequential
+    calls.  At n = 2^13 (c1) the same calls run unqueued."""
+    init_both(oracle, product, name)
+    rng = np.random.default_rng(11)
+    z1 = rng.uniform(-1, 1, oracle.slots) + 0j
+    z2 = rng.uniform(-1, 1, oracle.slots) + 0j
+    out = {}
+    for e in (oracle, product):
+        pk, sk, _, rlk = keys(e, rot=False)
+        a, b = e.encrypt(z1, pk), e.encrypt(z2, pk)
+        c = e.ct()
+        e.sub(c, a, b)
+        e.add(c, c, a)          # out aliases an input
+        e.neg(c)
+        d = e.ct()
+        e.copy_ct(d, c)
+        e.moddown(d)            # level drop between queued ops
+        g = e.ct()
+        e.add(g, d, a)          # mixed levels: min
+        e.free(c)               # c's block is free while ops naming it are queued
+        f = e.ct()
+        e.sub(f, a, b)          # queued user of the reused block
+        e.free(f)
+        h = e.ct()
+        e.mul(h, a, b, rlk)     # unqueued user of a reused block
+        pt = e.pt()
+        e.dec(pt, g, sk)
+        out[e.name] = [e.export(x) for x in (d, g, h, pt)] + [e.dcd(pt)]
+    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
+        assert np.array_equal(x, y), f"object {i} differs"
+    assert np.abs(out["product"][4] - (-(z1 - z2 + z1) + z1)).max() < 1e-6
