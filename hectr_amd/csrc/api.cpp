@@ -140,7 +140,7 @@ static void stage_release()
 // ===========================================================================
 struct PendEcd {
   uint64_t *dst;
-  unsigned lvl;
+  unsigned lvl, slots;
 };
 struct PendEnc {
   uint64_t *c0, *c1;
@@ -707,8 +707,17 @@ static void flush_pending()
   coef.swap(g_pcoef);
   const size_t n = G.n;
   if (!ecd.empty()) {
-    Ws dcoef(ecd.size() * n);
-    upload(dcoef.p, coef.data(), coef.size() * 8);
+    // an encoding of s slots is zero off the stride n / 2s: upload only the
+    // coefficients on the widest stride every queued encode shares
+    unsigned clog = G.logn;
+    for (const PendEcd &e : ecd)
+      clog = std::min(clog, (unsigned)__builtin_ctz(G.n / (2 * e.slots)));
+    const size_t row = n >> clog;
+    for (size_t i = 0; i < ecd.size(); i++)
+      for (size_t j = 0; j < row; j++)
+        coef[i * row + j] = coef[i * n + (j << clog)];
+    Ws dcoef(ecd.size() * row);
+    upload(dcoef.p, coef.data(), ecd.size() * row * 8);
     for (size_t i0 = 0; i0 < ecd.size();) {
       // one launch per run of equal levels (at most GPQHE_MAXGRP polys)
       size_t i1 = i0 + 1;
@@ -721,7 +730,7 @@ static void flush_pending()
       ls.ngp = (uint32_t)(i1 - i0);
       for (size_t i = i0; i < i1; i++)
         ls.gp[i - i0] = ecd[i].dst;
-      k_lift_ntt(ls, (const int64_t *)dcoef.p + i0 * n);
+      k_lift_ntt(ls, (const int64_t *)dcoef.p + i0 * row, clog);
       i0 = i1;
     }
   }
@@ -794,7 +803,7 @@ extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int s
     const size_t at = g_pcoef.size();
     g_pcoef.resize(at + G.n);
     hm_encode_coeffs(g_pcoef.data() + at, (const double *)z, slots, G.n, scale);
-    g_pecd.push_back({pt->data, nlimbs});
+    g_pecd.push_back({pt->data, nlimbs, slots});
   } else {
     unsigned mods[GPQHE_MAXMOD];
     for (unsigned i = 0; i < nlimbs; i++)

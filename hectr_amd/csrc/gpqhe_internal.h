@@ -279,7 +279,9 @@ void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);
 void k_lift_i64(const LimbSet &dst, const int64_t *coef);
-void k_lift_ntt(const LimbSet &dst, const int64_t *coef);  // lift + forward NTT (group g: coef + g n)
+// lift + forward NTT (group g: coef + g (n >> clog); clog > 0: only every
+// 2^clog-th coefficient is stored, the others are zero; n <= 2^12)
+void k_lift_ntt(const LimbSet &dst, const int64_t *coef, unsigned clog = 0);
 void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
                    const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl);
 // up to GPQHE_MAXGRP public-key encryptions in one launch: encryption i takes

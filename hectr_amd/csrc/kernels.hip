@@ -619,7 +619,7 @@ __device__ __forceinline__ void small_inv(const A &ar, uint64_t *lds, LD &&load,
 
 template <int LOGN, bool INV>
 __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs,
-                                                         const int64_t *coef, LimbSet in)
+                                                         const int64_t *coef, LimbSet in, unsigned clog)
 {
   constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
@@ -635,7 +635,13 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
       small_fwd<LOGN>(
           ar, lds,
           [&](int, int i) {
-            return A::load(coef ? lift_i64(coef[((size_t)(v / s.per) << LOGN) + i], mc) : xi[i]);
+            // coef: n >> clog values per group, coefficient i = j 2^clog holds
+            // value j, the others are 0
+            if (!coef)
+              return A::load(xi[i]);
+            return A::load((i & ((1 << clog) - 1))
+                               ? 0
+                               : lift_i64(coef[((size_t)(v / s.per) << (LOGN - clog)) + (i >> clog)], mc));
           },
           [&](int, int i, V a) { x[i] = ar.canon(a); });
     } else {
@@ -647,14 +653,16 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
 }
 
 // Encoding: lift the signed coefficients into every limb of s, then the
-// forward NTT (one launch for n <= 2^12).
-void k_lift_ntt(const LimbSet &s, const int64_t *coef)
+// forward NTT (one launch for n <= 2^12).  clog > 0 (n <= 2^12 only): each
+// group's row holds only every 2^clog-th coefficient (the others are zero:
+// an encoding of s slots has nonzero coefficients at stride n / 2s only).
+void k_lift_ntt(const LimbSet &s, const int64_t *coef, unsigned clog)
 {
   if (G.logn >= 10 && G.logn <= 12) {
     ProfScope ps(KC_NTT_SMALL_FWD, 8.0 * G.n * (s.count + 1));
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern, unsigned threads) {
-      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, coef, LimbSet{});
+      hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, coef, LimbSet{}, clog);
     };
     if (G.logn == 12)
       go(ntt_small_kernel<12, false>, 512);
@@ -665,6 +673,8 @@ void k_lift_ntt(const LimbSet &s, const int64_t *coef)
     HIP_CHECK(hipGetLastError());
     return;
   }
+  if (clog)
+    gpqhe_die("k_lift_ntt: strided coefficients need n <= 2^12");
   k_lift_i64(s, coef);
   k_ntt(s, false);
 }
@@ -678,7 +688,7 @@ static void ntt_small_launch(const LimbSet &s, const LimbSet &in, bool inverse)
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   auto go = [&](auto kern, unsigned threads) {
     hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, (const int64_t *)nullptr,
-                       in);
+                       in, 0u);
   };
   if (logn == 12)
     inverse ? go(ntt_small_kernel<12, true>, 512) : go(ntt_small_kernel<12, false>, 512);
@@ -2758,6 +2768,75 @@ __global__ void __launch_bounds__(512) moddown_small_kernel(uint64_t *out, uint6
   });
 }
 
+// The same ModDown in two launches when two or more limbs are dropped (the
+// batched he_gemv's / P q_top): the dropped limbs' inverse transforms run in
+// workgroups of their own, side by side, instead of one after another inside
+// one workgroup (the fused kernel's chain is nd + 1 transforms, this one's 2).
+// down_inv_small_kernel, grid (nd, npoly): Y[p][d] = INTT(X[p][keep + d])
+// [(D/d)^-1]_d, coefficient domain, canonical (the fused kernel's y).
+template <int LOGN>
+__global__ void __launch_bounds__(512) down_inv_small_kernel(uint64_t *Y, const uint64_t *X, size_t x_pstride,
+                                                              unsigned lvl, unsigned L, Tw2 tw, DownTable tab,
+                                                              const ModConst *mcs)
+{
+  __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN];
+  const unsigned d = blockIdx.x, p = blockIdx.y;
+  const unsigned bd = tab.keep + d, md = basis_mod(bd, lvl, L);
+  const ModConst mc = mcs[md];
+  const uint64_t *src = X + p * x_pstride + ((size_t)bd << LOGN);
+  uint64_t *y = Y + (((size_t)p * tab.nd + d) << LOGN);
+  const uint64_t yw = tab.y[d], ywp = tab.yp[d];
+  with_arith(mc.q, md, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_inv<LOGN>(
+        ar, lds, [&](int, int e) { return A::load(src[e]); },
+        [&](int, int e, typename A::V a) { y[e] = mul_shoup(ar.mulc(a, mc.ninv, mc.ninvp), yw, ywp, mc.q); });
+  });
+}
+
+// down_fwd_small_kernel, grid (keep, npoly): conversion sum of Y to slot t,
+// forward transform mod q_t, out = (X[t] - conv) [D^-1]_t, as the fused
+// kernel (thread th holds elements th + k n/8 before a forward transform).
+template <int LOGN>
+__global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint64_t *out2, unsigned half,
+                                                              size_t out_pstride, const uint64_t *Y,
+                                                              const uint64_t *X, size_t x_pstride, unsigned lvl,
+                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs)
+{
+  constexpr int n = 1 << LOGN;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned t = blockIdx.x, p = blockIdx.y;
+  const int th = threadIdx.x;
+  unsigned __int128 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    acc[k] = 0;
+  for (unsigned d = 0; d < tab.nd; d++) {
+    const uint64_t *y = Y + (((size_t)p * tab.nd + d) << LOGN);
+    const uint64_t cw = tab.c[(size_t)d * tab.keep + t];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      acc[k] += (unsigned __int128)y[th + k * (n / 8)] * cw;
+  }
+  const unsigned mt = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[mt];
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = redc128((uint64_t)(acc[k] >> 64), (uint64_t)acc[k], mc);
+  const uint64_t *xt = X + p * x_pstride + ((size_t)t << LOGN);
+  uint64_t *dst = (p < half ? out + p * out_pstride : out2 + (p - half) * out_pstride) + ((size_t)t << LOGN);
+  const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t];
+  with_arith(mc.q, mt, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds, [&](int k, int) { return A::load(r[k]); },
+        [&](int, int e, typename A::V a) {
+          dst[e] = mul_shoup(sub_mod(xt[e], ar.canon(a), mc.q), dinv, dinvp, mc.q);
+        });
+  });
+}
+
 // ModUp of NTT-domain inputs x1.p[0..count) (lvl limbs each, e.g. c1 of a
 // ciphertext, left unchanged) into D [count][ndig][nm] (NTT domain): one fused
 // launch for n <= 2^12, else copy + INTT + modup_kernel + NTT.
@@ -2816,10 +2895,29 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 {
   DownTable &tab = down_table(lvl, mode);
   if (G.logn >= 10 && G.logn <= 12) {
-    // one fused launch (moddown_small_kernel)
+    // one fused launch (moddown_small_kernel), or the inverse transforms of
+    // two or more dropped limbs in workgroups of their own first
     ProfScope ps(KC_DOWN_SMALL, 8.0 * G.n * npoly * (tab.nd + 2.0 * tab.keep));
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     const unsigned half = out2 ? npoly / 2 : npoly;
+    if (tab.nd >= 2) {
+      uint64_t *Y = (uint64_t *)pool_alloc(((size_t)npoly * tab.nd << G.logn) * 8);
+      auto go2 = [&](auto kinv, auto kfwd) {
+        hipLaunchKernelGGL(kinv, dim3(tab.nd, npoly), dim3(G.n / 8), 0, G.stream, Y, X, x_pstride, lvl, G.L, tw, tab,
+                           G.dev.mc);
+        hipLaunchKernelGGL(kfwd, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, Y,
+                           X, x_pstride, lvl, G.L, tw, tab, G.dev.mc);
+      };
+      if (G.logn == 12)
+        go2(down_inv_small_kernel<12>, down_fwd_small_kernel<12>);
+      else if (G.logn == 11)
+        go2(down_inv_small_kernel<11>, down_fwd_small_kernel<11>);
+      else
+        go2(down_inv_small_kernel<10>, down_fwd_small_kernel<10>);
+      HIP_CHECK(hipGetLastError());
+      pool_free(Y);
+      return;
+    }
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, X,
                          x_pstride, lvl, G.L, tw, tab, G.dev.mc);

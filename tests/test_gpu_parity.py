@@ -433,3 +433,28 @@ def test_ew_queue_sequences(oracle, product, name):
     for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
         assert np.array_equal(x, y), f"object {i} differs"
     assert np.abs(out["product"][4] - (-(z1 - z2 + z1) + z1)).max() < 1e-6
+
+
+def test_queued_encodes_mixed_slots(oracle, product):
+    """Queued he_ecd_ex at n = 4096 upload only the coefficients on the widest
+    stride all queued encodes share (api.cpp flush_pending, clog): 16, 2, 512
+    and 1 slots in one queue, then encryptions of them, bit-exact vs the
+    oracle."""
+    init_both(oracle, product, "ref")
+    rng = np.random.default_rng(4)
+    zs = [rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s) for s in (16, 2, 512, 1)]
+    out = {}
+    for e in (oracle, product):
+        pk, sk, _, _ = keys(e, rot=False)
+        pts, cts = [], []
+        for z in zs:
+            pt = e.pt()
+            e.ecd_ex(pt, z, len(z), e.info.delta, e.L)
+            pts.append(pt)
+        for pt in pts:
+            ct = e.ct()
+            e.enc_pk(ct, pt, pk)
+            cts.append(ct)
+        out[e.name] = [e.export(x) for x in pts + cts]
+    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
+        assert np.array_equal(x, y), f"object {i} differs"
