@@ -95,7 +95,8 @@ struct Stage {
 static Stage g_stage[8];
 static unsigned g_stage_next = 0;
 
-static void upload(void *dst, const void *src, size_t bytes)
+// The next slot, free again (its last reader has run), holding a copy of src.
+static Stage &stage_fill(const void *src, size_t bytes)
 {
   Stage &s = g_stage[g_stage_next++ % 8];
   if (s.ev)
@@ -109,12 +110,38 @@ static void upload(void *dst, const void *src, size_t bytes)
     s.bytes = bytes;
   }
   memcpy(s.host, src, bytes);
+  return s;
+}
+
+static void upload(void *dst, const void *src, size_t bytes)
+{
+  Stage &s = stage_fill(src, bytes);
   HIP_CHECK(hipMemcpyAsync(dst, s.host, bytes, hipMemcpyHostToDevice, G.stream));
   HIP_CHECK(hipEventRecord(s.ev, G.stream));
 }
 
+// Zero-copy form for a few KB that one launch reads: the kernel reads the
+// pinned slot over PCIe (no copy launch); stage_done() after that launch.
+static Stage &stage_map(const void *src, size_t bytes, const void **dev)
+{
+  Stage &s = stage_fill(src, bytes);
+  void *d = nullptr;
+  HIP_CHECK(hipHostGetDevicePointer(&d, s.host, 0));
+  *dev = d;
+  return s;
+}
+
+static void stage_done(Stage &s) { HIP_CHECK(hipEventRecord(s.ev, G.stream)); }
+
+static void *g_zpin = nullptr;  // pinned decode output (he_dcd_ex)
+static size_t g_zpin_bytes = 0;
+
 static void stage_release()
 {
+  if (g_zpin)
+    (void)hipHostFree(g_zpin);
+  g_zpin = nullptr;
+  g_zpin_bytes = 0;
   for (Stage &s : g_stage) {
     if (s.ev) {
       (void)hipEventSynchronize(s.ev);
@@ -716,8 +743,17 @@ static void flush_pending()
     for (size_t i = 0; i < ecd.size(); i++)
       for (size_t j = 0; j < row; j++)
         coef[i * row + j] = coef[i * n + (j << clog)];
-    Ws dcoef(ecd.size() * row);
-    upload(dcoef.p, coef.data(), ecd.size() * row * 8);
+    // up to CoefArg::MAX values (HECTR's step: 5 x 32) they travel in the
+    // kernel arguments; up to 64 KB the lift kernels read them straight from
+    // pinned host memory; more is uploaded first
+    const size_t cbytes = ecd.size() * row * 8;
+    const bool arg = ecd.size() * row <= CoefArg::MAX, zc = !arg && cbytes <= 65536;
+    Ws up(arg || zc ? 0 : ecd.size() * row);
+    const void *dmap = up.p;
+    Stage *st = zc ? &stage_map(coef.data(), cbytes, &dmap) : nullptr;
+    if (!arg && !zc)
+      upload(up.p, coef.data(), cbytes);
+    const int64_t *dcoef = (const int64_t *)dmap;
     for (size_t i0 = 0; i0 < ecd.size();) {
       // one launch per run of equal levels (at most GPQHE_MAXGRP polys)
       size_t i1 = i0 + 1;
@@ -730,9 +766,14 @@ static void flush_pending()
       ls.ngp = (uint32_t)(i1 - i0);
       for (size_t i = i0; i < i1; i++)
         ls.gp[i - i0] = ecd[i].dst;
-      k_lift_ntt(ls, (const int64_t *)dcoef.p + i0 * row, clog);
+      if (arg)
+        k_lift_ntt_arg(ls, coef.data() + i0 * row, clog);
+      else
+        k_lift_ntt(ls, dcoef + i0 * row, clog);
       i0 = i1;
     }
+    if (st)
+      stage_done(*st);
   }
   for (size_t i0 = 0; i0 < enc.size();) {
     // a run of encryptions at one level with consecutive RNG streams and the
@@ -832,10 +873,27 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     k_ntt_ex(qlimbs(pt->data, nl, 1, words), qlimbs(c.p, nl, 1, words), true, nullptr);
     src = c.p;
   }
-  // CRT lift + FFT on the GPU (k_decode); only the s values cross PCIe
+  // CRT lift + FFT on the GPU (k_decode); only the s values cross PCIe,
+  // written by the kernel straight into pinned host memory when one launch
+  // does it (no copy launch)
+  const size_t zb = (size_t)slots * 16;
+  if (slots <= GPQHE_DCD_ONEPASS) {
+    if (g_zpin_bytes < zb) {
+      if (g_zpin)
+        HIP_CHECK(hipHostFree(g_zpin));
+      HIP_CHECK(hipHostMalloc(&g_zpin, zb, hipHostMallocDefault));
+      g_zpin_bytes = zb;
+    }
+    void *dz = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&dz, g_zpin, 0));
+    k_decode((double *)dz, src, nl, slots, pt->scale);
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+    memcpy(z, g_zpin, zb);
+    return;
+  }
   Ws zd(2 * (size_t)slots);
   k_decode((double *)zd.p, src, nl, slots, pt->scale);
-  HIP_CHECK(hipMemcpyAsync(z, zd.p, (size_t)slots * 16, hipMemcpyDeviceToHost, G.stream));
+  HIP_CHECK(hipMemcpyAsync(z, zd.p, zb, hipMemcpyDeviceToHost, G.stream));
   HIP_CHECK(hipStreamSynchronize(G.stream));
 }
 

@@ -236,6 +236,9 @@ void hm_encode_coeffs(int64_t *coef, const double *z_interleaved, unsigned s, un
 // GPU decoder: z (device, s complex values) <- the centred CRT lift of the
 // coefficient limbs coef [nl][n] (device), / scale, forward special FFT --
 // bit-identical to the oracle's he_dcd; asynchronous on the engine stream.
+// Up to GPQHE_DCD_ONEPASS slots one launch writes each value of z once, so z
+// may be mapped pinned host memory.
+#define GPQHE_DCD_ONEPASS 2048u
 void k_decode(double *z, const uint64_t *coef, unsigned nl, unsigned s, double scale);
 
 // ---------------------------------------------------------------------------
@@ -282,6 +285,14 @@ void k_lift_i64(const LimbSet &dst, const int64_t *coef);
 // lift + forward NTT (group g: coef + g (n >> clog); clog > 0: only every
 // 2^clog-th coefficient is stored, the others are zero; n <= 2^12)
 void k_lift_ntt(const LimbSet &dst, const int64_t *coef, unsigned clog = 0);
+// The same with at most CoefArg::MAX coefficients in total (host memory,
+// n >> clog per group), passed to the kernel by value (n <= 2^12).
+struct CoefArg {
+  static constexpr unsigned MAX = 320;
+  int64_t v[MAX];
+  unsigned clog, row;
+};
+void k_lift_ntt_arg(const LimbSet &dst, const int64_t *coef_host, unsigned clog);
 void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t *e0, const uint64_t *e1,
                    const uint64_t *pk0, const uint64_t *pk1, const uint64_t *m, unsigned lvl);
 // up to GPQHE_MAXGRP public-key encryptions in one launch: encryption i takes

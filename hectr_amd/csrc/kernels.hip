@@ -652,6 +652,52 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
   });
 }
 
+// The same lift + forward transform with the (few) coefficients passed by
+// value in the kernel arguments: group g's value j at ca.v[g row + j] is
+// coefficient j 2^clog, the others are 0.  No upload, no host-memory reads.
+template <int LOGN>
+__global__ void __launch_bounds__(512) lift_ntt_arg_kernel(LimbSet s, Tw2 tw, const ModConst *mcs, CoefArg ca)
+{
+  constexpr int n = 1 << LOGN;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned v = blockIdx.x;
+  uint64_t *x = s.limb(v, LOGN);
+  const unsigned m = s.mod(v), g = v / s.per, clog = ca.clog;
+  const ModConst mc = mcs[m];
+  with_arith(mc.q, m, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds,
+        [&](int, int i) {
+          return A::load((i & ((1 << clog) - 1)) ? 0 : lift_i64(ca.v[g * ca.row + (i >> clog)], mc));
+        },
+        [&](int, int i, typename A::V a) { x[i] = ar.canon(a); });
+  });
+}
+
+void k_lift_ntt_arg(const LimbSet &s, const int64_t *coef_host, unsigned clog)
+{
+  const unsigned row = G.n >> clog, groups = s.count / s.per;
+  if (G.logn < 10 || G.logn > 12 || (size_t)groups * row > CoefArg::MAX)
+    gpqhe_die("k_lift_ntt_arg: %u x %u coefficients at n = %u", groups, row, G.n);
+  CoefArg ca;
+  memcpy(ca.v, coef_host, (size_t)groups * row * 8);
+  ca.clog = clog;
+  ca.row = row;
+  ProfScope ps(KC_NTT_SMALL_FWD, 8.0 * G.n * s.count);
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  auto go = [&](auto kern, unsigned threads) {
+    hipLaunchKernelGGL(kern, dim3(s.count), dim3(threads), 0, G.stream, s, tw, G.dev.mc, ca);
+  };
+  if (G.logn == 12)
+    go(lift_ntt_arg_kernel<12>, 512);
+  else if (G.logn == 11)
+    go(lift_ntt_arg_kernel<11>, 256);
+  else
+    go(lift_ntt_arg_kernel<10>, 128);
+  HIP_CHECK(hipGetLastError());
+}
+
 // Encoding: lift the signed coefficients into every limb of s, then the
 // forward NTT (one launch for n <= 2^12).  clog > 0 (n <= 2^12 only): each
 // group's row holds only every 2^clog-th coefficient (the others are zero:
@@ -1069,6 +1115,7 @@ void k_sample_uniform(const LimbSet &dst, uint64_t stream)
 //   in LDS (the chunks are independent below that length).
 // ---------------------------------------------------------------------------
 constexpr unsigned FFT_LDS = 2048;
+static_assert(FFT_LDS == GPQHE_DCD_ONEPASS, "k_decode's one-launch bound");
 
 __device__ __forceinline__ void fft_enc_bfly(double2 &x, double2 &y, const double2 w)
 {

@@ -435,14 +435,17 @@ def test_ew_queue_sequences(oracle, product, name):
     assert np.abs(out["product"][4] - (-(z1 - z2 + z1) + z1)).max() < 1e-6
 
 
-def test_queued_encodes_mixed_slots(oracle, product):
-    """Queued he_ecd_ex at n = 4096 upload only the coefficients on the widest
-    stride all queued encodes share (api.cpp flush_pending, clog): 16, 2, 512
-    and 1 slots in one queue, then encryptions of them, bit-exact vs the
-    oracle."""
+@pytest.mark.parametrize("slot_set", [(16,) * 5, (16, 2, 512, 1), (1024,) * 5],
+                         ids=["kernel_args", "pinned_map", "upload"])
+def test_queued_encodes_mixed_slots(oracle, product, slot_set):
+    """Queued he_ecd_ex at n = 4096 pass only the coefficients on the widest
+    stride all queued encodes share (api.cpp flush_pending, clog), in the
+    kernel arguments (HECTR's 5 x 16 slots), read from pinned host memory
+    (16, 2, 512 and 1 slots: 4 x 1024 values) or uploaded (5 x 1024 slots),
+    then encryptions of them, bit-exact vs the oracle."""
     init_both(oracle, product, "ref")
     rng = np.random.default_rng(4)
-    zs = [rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s) for s in (16, 2, 512, 1)]
+    zs = [rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s) for s in slot_set]
     out = {}
     for e in (oracle, product):
         pk, sk, _, _ = keys(e, rot=False)
