@@ -861,8 +861,39 @@ extern "C" void he_ecd(he_pt_t *pt, const gpqhe_complex_t z[])
   he_ecd_ex(pt, z, G.slots, G.delta, G.L);
 }
 
+static void *zpin(size_t bytes)
+{
+  if (g_zpin_bytes < bytes) {
+    if (g_zpin)
+      HIP_CHECK(hipHostFree(g_zpin));
+    HIP_CHECK(hipHostMalloc(&g_zpin, bytes, hipHostMallocDefault));
+    g_zpin_bytes = bytes;
+  }
+  void *dz = nullptr;
+  HIP_CHECK(hipHostGetDevicePointer(&dz, g_zpin, 0));
+  return dz;
+}
+
 extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
 {
+  const size_t zb = (size_t)slots * 16;
+  if (G.init && defer_ok(0) && slots && !(slots & (slots - 1)) && slots <= GPQHE_DCD_ONEPASS &&
+      slots <= G.n / 2 && !(pt->flags & GPQHE_F_COEFF) && pt->nlimbs >= 1 && pt->nlimbs <= 2) {
+    // the small-N step's tail: the queued elementwise program (he_add, he_neg,
+    // he_copy_ct, he_add, he_dec), the inverse transform and the decoder in
+    // one launch (k_ew_decode)
+    if (!g_pgemv.empty())
+      flush_gemvs();
+    if (!g_pecd.empty() || !g_penc.empty())
+      flush_pending();
+    const EwProg p = g_pew;
+    g_pew.count = 0;
+    Ws c((size_t)pt->nlimbs << G.logn);
+    k_ew_decode(p, (double *)zpin(zb), pt->data, pt->nlimbs, slots, pt->scale, c.p);
+    HIP_CHECK(hipStreamSynchronize(G.stream));
+    memcpy(z, g_zpin, zb);
+    return;
+  }
   check_ctx();
   const unsigned nl = pt->nlimbs;
   const size_t words = (size_t)nl << G.logn;
@@ -876,17 +907,8 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
   // CRT lift + FFT on the GPU (k_decode); only the s values cross PCIe,
   // written by the kernel straight into pinned host memory when one launch
   // does it (no copy launch)
-  const size_t zb = (size_t)slots * 16;
   if (slots <= GPQHE_DCD_ONEPASS) {
-    if (g_zpin_bytes < zb) {
-      if (g_zpin)
-        HIP_CHECK(hipHostFree(g_zpin));
-      HIP_CHECK(hipHostMalloc(&g_zpin, zb, hipHostMallocDefault));
-      g_zpin_bytes = zb;
-    }
-    void *dz = nullptr;
-    HIP_CHECK(hipHostGetDevicePointer(&dz, g_zpin, 0));
-    k_decode((double *)dz, src, nl, slots, pt->scale);
+    k_decode((double *)zpin(zb), src, nl, slots, pt->scale);
     HIP_CHECK(hipStreamSynchronize(G.stream));
     memcpy(z, g_zpin, zb);
     return;

@@ -278,6 +278,10 @@ struct EwProg {
   unsigned count;
 };
 void k_ew_prog(const EwProg &p);
+// k_ew_prog(p), then he_dcd of the NTT-form plaintext pt (nl <= 2 limbs,
+// s <= GPQHE_DCD_ONEPASS, n = 2^10 .. 2^12) in one more launch; c: nl n
+// words of workspace; z as k_decode's.
+void k_ew_decode(const EwProg &p, double *z, const uint64_t *pt, unsigned nl, unsigned s, double scale, uint64_t *c);
 void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);

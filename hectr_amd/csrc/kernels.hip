@@ -1334,14 +1334,14 @@ __device__ double dcd_crt_center(const uint64_t *c, unsigned k, unsigned nl, uns
   return neg ? -d : d;
 }
 
+// One chunk of len0 elements at base: lift into sh, stages 2 .. len0, store.
 template <int NLM>
-__global__ void __launch_bounds__(512) fft_dec_lds_kernel(double2 *v, const uint64_t *c, unsigned nl, unsigned logn,
-                                                          unsigned s, unsigned logs, unsigned len0, double scale,
-                                                          const ModConst *mc, const uint64_t *ginv, unsigned ld,
-                                                          const double2 *ksi, const unsigned *rot)
+__device__ __forceinline__ void dcd_chunk(double2 *sh, double2 *v, unsigned base, const uint64_t *c, unsigned nl,
+                                          unsigned logn, unsigned s, unsigned logs, unsigned len0, double scale,
+                                          const ModConst *mc, const uint64_t *ginv, unsigned ld, const double2 *ksi,
+                                          const unsigned *rot)
 {
-  __shared__ double2 sh[FFT_LDS];
-  const unsigned base = blockIdx.x * len0, M = 4 * s, gap = (1u << logn) / (2 * s);
+  const unsigned M = 4 * s, gap = (1u << logn) / (2 * s);
   for (unsigned e = threadIdx.x; e < len0; e += blockDim.x) {
     const unsigned slot = logs ? __brev(base + e) >> (32 - logs) : 0;  // v = bit-reversed u
     const double re = dcd_crt_center<NLM>(c, slot * gap, nl, logn, mc, ginv, ld);
@@ -1361,6 +1361,16 @@ __global__ void __launch_bounds__(512) fft_dec_lds_kernel(double2 *v, const uint
     v[base + e] = sh[e];
 }
 
+template <int NLM>
+__global__ void __launch_bounds__(512) fft_dec_lds_kernel(double2 *v, const uint64_t *c, unsigned nl, unsigned logn,
+                                                          unsigned s, unsigned logs, unsigned len0, double scale,
+                                                          const ModConst *mc, const uint64_t *ginv, unsigned ld,
+                                                          const double2 *ksi, const unsigned *rot)
+{
+  __shared__ double2 sh[FFT_LDS];
+  dcd_chunk<NLM>(sh, v, blockIdx.x * len0, c, nl, logn, s, logs, len0, scale, mc, ginv, ld, ksi, rot);
+}
+
 __global__ void fft_dec_stage_kernel(double2 *v, unsigned s, unsigned len, const double2 *ksi, const unsigned *rot)
 {
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1373,20 +1383,26 @@ __global__ void fft_dec_stage_kernel(double2 *v, unsigned s, unsigned len, const
 
 static uint64_t *g_ginv = nullptr;  // [L][L] Garner inverses of the current context
 
+static void garner_table()
+{
+  if (g_ginv)
+    return;
+  const unsigned ld = G.L;
+  std::vector<uint64_t> h((size_t)ld * ld, 0);
+  for (unsigned i = 0; i < ld; i++)
+    for (unsigned j = 0; j < i; j++)
+      h[(size_t)i * ld + j] = hm_inv_mod(G.q[j] % G.q[i], G.q[i]);
+  HIP_CHECK(hipMalloc(&g_ginv, h.size() * 8));
+  HIP_CHECK(hipMemcpy(g_ginv, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+}
+
 void k_decode(double *z, const uint64_t *coef, unsigned nl, unsigned s, double scale)
 {
   const FftDev &T = fft_dev(s);
   if (nl < 1 || nl > G.L)
     gpqhe_die("he_dcd: bad level %u", nl);
   const unsigned ld = G.L;
-  if (!g_ginv) {
-    std::vector<uint64_t> h((size_t)ld * ld, 0);
-    for (unsigned i = 0; i < ld; i++)
-      for (unsigned j = 0; j < i; j++)
-        h[(size_t)i * ld + j] = hm_inv_mod(G.q[j] % G.q[i], G.q[i]);
-    HIP_CHECK(hipMalloc(&g_ginv, h.size() * 8));
-    HIP_CHECK(hipMemcpy(g_ginv, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-  }
+  garner_table();
   double2 *v = (double2 *)z;
   const unsigned logs = (unsigned)__builtin_ctz(s), len0 = std::min(s, FFT_LDS);
   const dim3 grid(s / len0), block(std::min(512u, std::max(64u, len0 / 2)));
@@ -1407,6 +1423,61 @@ void k_decode(double *z, const uint64_t *coef, unsigned nl, unsigned s, double s
   for (unsigned len = 2 * len0; len <= s; len <<= 1)
     hipLaunchKernelGGL(fft_dec_stage_kernel, dim3((s / 2 + TPB - 1) / TPB), dim3(TPB), 0, G.stream, v, s, len,
                        T.ksi, T.rot);
+  HIP_CHECK(hipGetLastError());
+}
+
+// The decoder's tail of a small-N control step: the inverse transform of the
+// plaintext's nl <= 2 limbs and the decoder (s <= FFT_LDS) in one workgroup,
+// which reads what it wrote after a barrier.  Same values as
+// ntt_small_kernel<inv> + fft_dec_lds_kernel.  Measured non-levers: the
+// queued elementwise program inside this workgroup too (one CU streams the
+// program's ~1.2 MB: 44 us against 19 us for the three launches), and the
+// transforms in one workgroup per limb with the last one to finish decoding
+// (the agent-scope release / acquire that hand-off needs: 42 us).
+template <int LOGN>
+__global__ void __launch_bounds__(512) inv_dcd_kernel(const uint64_t *pt, unsigned nl, uint64_t *c, double2 *z,
+                                                       unsigned s, unsigned logs, double scale, Tw2 tw,
+                                                       const ModConst *mcs, const uint64_t *ginv, unsigned ld,
+                                                       const double2 *ksi, const unsigned *rot)
+{
+  constexpr int n = 1 << LOGN;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  for (unsigned l = 0; l < nl; l++) {
+    __syncthreads();  // the previous transform's LDS use
+    const ModConst mc = mcs[l];
+    const uint64_t *xi = pt + ((size_t)l << LOGN);
+    uint64_t *x = c + ((size_t)l << LOGN);
+    with_arith(mc.q, l, LOGN, tw, [&](const auto &ar) {
+      using A = std::decay_t<decltype(ar)>;
+      small_inv<LOGN>(
+          ar, lds, [&](int, int i) { return A::load(xi[i]); },
+          [&](int, int i, typename A::V a) { x[i] = ar.mulc(a, mc.ninv, mc.ninvp); });
+    });
+  }
+  __syncthreads();
+  dcd_chunk<2>((double2 *)lds, z, 0, c, nl, LOGN, s, logs, s, scale, mcs, ginv, ld, ksi, rot);
+}
+
+void k_ew_decode(const EwProg &p, double *z, const uint64_t *pt, unsigned nl, unsigned s, double scale, uint64_t *c)
+{
+  const FftDev &T = fft_dev(s);
+  if (nl < 1 || nl > 2 || nl > G.L || s > FFT_LDS || G.logn < 10 || G.logn > 12)
+    gpqhe_die("k_ew_decode: n = %u, %u limbs, %u slots", G.n, nl, s);
+  garner_table();
+  const unsigned logs = (unsigned)__builtin_ctz(s);
+  k_ew_prog(p);
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  ProfScope ps(KC_NTT_SMALL_INV, 16.0 * G.n * nl);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(1), dim3(G.n / 8), 0, G.stream, pt, nl, c, (double2 *)z, s, logs, scale, tw,
+                       G.dev.mc, g_ginv, G.L, T.ksi, T.rot);
+  };
+  if (G.logn == 12)
+    go(inv_dcd_kernel<12>);
+  else if (G.logn == 11)
+    go(inv_dcd_kernel<11>);
+  else
+    go(inv_dcd_kernel<10>);
   HIP_CHECK(hipGetLastError());
 }
 

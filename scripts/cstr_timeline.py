@@ -26,8 +26,8 @@ ev.sort()
 print("files:", [os.path.relpath(f, d) for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True)])
 print("copy kinds:", sorted({e[3] for e in ev if e[2] == "C"}))
 ends = [i for i, e in enumerate(ev) if e[2] == "C" and "DEVICE_TO_HOST" in e[3].upper()]
-if len(ends) < 4:  # no copy trace: the decoder's last kernel ends each step
-    ends = [i for i, e in enumerate(ev) if e[2] == "K" and e[3].startswith("void fft_dec")]
+if len(ends) < 4:  # no D2H copy: the decoder's kernel ends each step
+    ends = [i for i, e in enumerate(ev) if e[2] == "K" and ("fft_dec" in e[3] or "inv_dcd" in e[3])]
 steps = []
 for a, b in zip(ends[:-1], ends[1:]):
     seg = ev[a + 1:b + 1]
