@@ -80,7 +80,7 @@ void pool_release_all()
 // RAII workspace
 struct Ws {
   uint64_t *p;
-  explicit Ws(size_t words) : p((uint64_t *)pool_alloc(words * 8)) {}
+  explicit Ws(size_t words) : p(words ? (uint64_t *)pool_alloc(words * 8) : nullptr) {}
   ~Ws() { pool_free(p); }
   Ws(const Ws &) = delete;
   Ws &operator=(const Ws &) = delete;

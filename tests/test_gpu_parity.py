@@ -461,3 +461,37 @@ def test_queued_encodes_mixed_slots(oracle, product, slot_set):
         out[e.name] = [e.export(x) for x in pts + cts]
     for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
         assert np.array_equal(x, y), f"object {i} differs"
+
+
+@pytest.mark.parametrize("name", ["ref", "c1"])
+def test_plaintext_ops_rot0_and_queue_overflow(oracle, product, name):
+    """he_add_pt (out != a: a queued copy the add then reads; and in place),
+    he_mul_pt, he_rot by 0 (a queued copy at n <= 2^12), and a chain of 20
+    he_add calls (40 queued entries: the elementwise queue runs whenever 16
+    fill up) -- bit-exact vs the oracle."""
+    init_both(oracle, product, name)
+    rng = np.random.default_rng(21)
+    s = oracle.slots
+    z1 = rng.uniform(-1, 1, s) + 0j
+    z2 = rng.uniform(-1, 1, s) + 0j
+    res = {}
+    for e in (oracle, product):
+        pk, sk, rk, _ = keys(e)
+        a = e.encrypt(z1, pk)
+        pt = e.pt()
+        e.ecd(pt, z2)
+        out = {}
+        c = e.ct(); e.add_pt(c, a, pt); out["add_pt"] = c
+        c = e.ct(); e.copy_ct(c, a); e.add_pt(c, c, pt); out["add_pt_inplace"] = c
+        c = e.ct(); e.mul_pt(c, a, pt); out["mul_pt"] = c
+        c = e.ct(); e.rot(c, a, 0, rk); out["rot0"] = c
+        c = e.ct(); e.copy_ct(c, a)
+        for _ in range(20):
+            e.add(c, c, a)
+        out["add_chain"] = c
+        res[e.name] = {k: e.export(v) for k, v in out.items()}
+        if e is product:
+            assert np.abs(e.decrypt(out["add_chain"], sk) - 21 * z1).max() < 1e-5
+            assert np.abs(e.decrypt(out["add_pt"], sk) - (z1 + z2)).max() < 1e-6
+    for k in res["oracle"]:
+        assert np.array_equal(res["oracle"][k], res["product"][k]), k
