@@ -305,8 +305,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
   });
 }
 
-template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW, bool KEEP>
-static void ksq_launch(const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
+template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW>
+static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
                        size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl,
                        unsigned nm, unsigned t_lo, unsigned t_n)
 {
@@ -320,15 +320,15 @@ static void ksq_launch(const uint64_t *T1, const D01Src &d01, const uint64_t *ev
     members++;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const size_t t1_stride = (size_t)NDIG * nm * n;
-  auto kern = ksq_kernel<LOGN2, NDIG, QN, ALLF, KEEP, LTW>;
+  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, LTW>;
   hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, T1, t1_stride, d01, evkm,
                      dst, dst_pstride, conv, dinv, dinvp, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
                      members, t_lo, t_n, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
-template <int LOGN2, bool KEEP>
-static void ksq_dispatch(unsigned ndig, bool allf, const uint64_t *T1, const D01Src &d01,
+template <int LOGN2>
+static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
                          const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv,
                          const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo,
                          unsigned t_n)
@@ -339,14 +339,14 @@ static void ksq_dispatch(unsigned ndig, bool allf, const uint64_t *T1, const D01
   case 1:
     // two streams (256 VGPRs); four (1024 threads, 128 VGPRs) spilled 58-193:
     // 68.2k -> 77.6k ct-mult/s at N=2^16, L=4, dnum=1 (same box)
-    ksq_launch<LOGN2, 1, 2, false, true, KEEP>(T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    ksq_launch<LOGN2, 1, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
     if (allf)
-      ksq_launch<LOGN2, 2, 3, true, true, KEEP>(T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+      ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
     else  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk, 60-bit set)
-      ksq_launch<LOGN2, 2, 2, false, true, KEEP>(T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
                                            t_lo, t_n);
     break;
   case 3:
@@ -354,50 +354,32 @@ static void ksq_dispatch(unsigned ndig, bool allf, const uint64_t *T1, const D01
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
     if (allf)
-      ksq_launch<LOGN2, 3, 2, true, false, KEEP>(T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
                                            t_lo, t_n);
     else
-      ksq_launch<LOGN2, 3, 2, false, false, KEEP>(T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 3, 2, false, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
                                             t_lo, t_n);
     break;
   default: gpqhe_die("split key switch: %u digits", ndig);
   }
 }
 
-// The kept slots' kernels are compiled in a translation unit of their own
-// (KSQ_KEEP=1, Makefile: ks_split_keep.o) with the register-minimising
-// scheduler: the three-stream kept-slot kernel then fits 162 VGPRs without
-// spills (the default schedule spilled 7-9 at the 168 that three 256-thread
-// streams allow); the dropped slots' kernels keep the default schedule.
-#define KSQ_ARGS                                                                                                \
-  unsigned logn2, unsigned ndig, bool allf, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm,        \
-      uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp,     \
-      unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n
-#define KSQ_PASS ndig, allf, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n
-
-template <bool KEEP>
-static void ksq_stage(KSQ_ARGS)
-{
-  switch (logn2) {
-  case 7: ksq_dispatch<7, KEEP>(KSQ_PASS); break;
-  case 8: ksq_dispatch<8, KEEP>(KSQ_PASS); break;
-  case 9: ksq_dispatch<9, KEEP>(KSQ_PASS); break;
-  default: gpqhe_die("split key switch: row length 2^%u", logn2);
-  }
-}
-
-void ksq_run_keep(KSQ_ARGS);
-
-#if KSQ_KEEP
-void ksq_run_keep(KSQ_ARGS) { ksq_stage<true>(logn2, KSQ_PASS); }
-#else
 void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
              const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv,
              const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
 {
-  if (keep_stage)
-    ksq_run_keep(logn2, KSQ_PASS);
-  else
-    ksq_stage<false>(logn2, KSQ_PASS);
-}
+#ifdef KSQ_DEV  // analysis builds: the bench's instantiations only
+  if (logn2 == 8 && ndig == 2 && allf) {
+    ksq_launch<8, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    return;
+  }
+  gpqhe_die("KSQ_DEV build");
+#else
+  switch (logn2) {
+  case 7: ksq_dispatch<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  case 8: ksq_dispatch<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  case 9: ksq_dispatch<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  default: gpqhe_die("split key switch: row length 2^%u", logn2);
+  }
 #endif
+}
