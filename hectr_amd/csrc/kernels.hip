@@ -371,7 +371,8 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 // forward ones), instead of every tile re-fetching its 20 twiddle pairs per
 // thread from L2.
 // (launch bound: two workgroups per CU; the inverse then spills 16 VGPRs
-// but the roundtrip runs 7.55 -> 7.45 ms, same box)
+// but the roundtrip runs 7.55 -> 7.45 ms, same box; the inverse alone at one
+// workgroup per CU, no spills, ran 7.39 -> 7.50 ms)
 template <int LOGN2, bool INV, int QN>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                              const ModConst *mcs, unsigned members)
