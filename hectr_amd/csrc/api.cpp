@@ -202,21 +202,17 @@ static std::vector<PendGemv> g_pgemv;
 // every writer outside this queue flushes it first.  The three queues are
 // never non-empty at once.
 static EwProg g_pew{};
-static std::vector<void *> g_pew_keep;  // workspaces queued ops read (freed once launched)
 
-static void flush_pending(bool keep_ew = false);
+static void flush_pending();
 static void flush_gemvs();
 
 static void flush_ew()
 {
-  if (g_pew.count) {
-    const EwProg p = g_pew;
-    g_pew.count = 0;
-    k_ew_prog(p);
-  }
-  for (void *b : g_pew_keep)
-    pool_free(b);  // stream-ordered: after the launch that reads it
-  g_pew_keep.clear();
+  if (!g_pew.count)
+    return;
+  const EwProg p = g_pew;
+  g_pew.count = 0;
+  k_ew_prog(p);
 }
 
 static void check_ctx()
@@ -728,10 +724,7 @@ static bool defer_ok(unsigned s)
   return on && G.logn <= 12 && G.logn >= 10 && s < gpu_ecd_min();
 }
 
-// keep_ew: the encryptions' combine step stays queued as elementwise ops
-// (EW_ENC0 / EW_DEC), so the calls that queue elementwise work next (HECTR's
-// he_sub x2, src/hempc.c:253-256) join the same launch; otherwise it runs now.
-static void flush_pending(bool keep_ew)
+static void flush_pending()
 {
   std::vector<PendEcd> ecd;
   std::vector<PendEnc> enc;
@@ -794,24 +787,19 @@ static void flush_pending(bool keep_ew)
     unsigned mods[GPQHE_MAXMOD];
     for (unsigned l = 0; l < lvl; l++)
       mods[l] = l;
-    uint64_t *vee = (uint64_t *)pool_alloc(3 * k * w * 8);
-    LimbSet s = limbset(vee, mods, lvl, 3 * k, w);
+    Ws vee(3 * k * w);
+    LimbSet s = limbset(vee.p, mods, lvl, 3 * k, w);
     k_sample_enc(s, enc[i0].stream, 3 * k);
     k_ntt(s, false);
-    // c0 = (e0 + v pk0) + m, c1 = e1 + v pk1 (enc_batch_kernel's values) as
-    // queued elementwise ops; vee lives until they have been launched
-    if (g_pew.count + 2 * k > EwProg::MAX)
-      flush_ew();
+    EncBatch b{};
     for (unsigned e = 0; e < k; e++) {
-      const uint64_t *v = vee + 3 * e * w;
-      g_pew.op[g_pew.count++] = EwOp{enc[i0 + e].c0, v + w, v, enc[i0].pk0, enc[i0 + e].m, EW_ENC0, lvl};
-      g_pew.op[g_pew.count++] = EwOp{enc[i0 + e].c1, v + 2 * w, v, enc[i0].pk1, nullptr, EW_DEC, lvl};
+      b.c0[e] = enc[i0 + e].c0;
+      b.c1[e] = enc[i0 + e].c1;
+      b.m[e] = enc[i0 + e].m;
     }
-    g_pew_keep.push_back(vee);
+    k_enc_combine_batch(b, k, vee.p, enc[i0].pk0, enc[i0].pk1, lvl);
     i0 = i1;
   }
-  if (!keep_ew)
-    flush_ew();
 }
 
 static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scale, const unsigned *mods,
@@ -1007,7 +995,7 @@ static bool ew_defer(unsigned nops)
   if (!g_pgemv.empty())
     flush_gemvs();
   if (!g_pecd.empty() || !g_penc.empty())
-    flush_pending(true);  // the encryptions' combine joins this program
+    flush_pending();
   if (g_pew.count + nops > EwProg::MAX)
     flush_ew();
   return true;
@@ -1016,7 +1004,7 @@ static bool ew_defer(unsigned nops)
 static void ew_push(uint32_t kind, uint64_t *out, const uint64_t *a, const uint64_t *b, const uint64_t *sk,
                     unsigned lvl)
 {
-  g_pew.op[g_pew.count++] = EwOp{out, a, b, sk, nullptr, kind, lvl};
+  g_pew.op[g_pew.count++] = EwOp{out, a, b, sk, kind, lvl};
 }
 
 extern "C" void he_dec(he_pt_t *pt, const he_ct_t *ct, const poly_mpi_t *sk)

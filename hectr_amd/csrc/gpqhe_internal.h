@@ -264,13 +264,12 @@ void k_tensor(uint64_t *d01, uint64_t *d2, const uint64_t *a, const uint64_t *b,
 void k_dec(uint64_t *pt, const uint64_t *c0, const uint64_t *c1, const uint64_t *s, unsigned lvl);
 // Deferred elementwise program (the small-N latency path, api.cpp): queued
 // he_add / he_sub / he_neg / he_copy_ct / he_dec polys, applied in queue order
-// to every element (limb, k) by one launch.  Op: out = a + b, a - b, -a, a,
-// a + b s (decryption: a = c0, b = c1, s = the secret key; and c1 = e1 + v pk1
-// of a queued encryption), or (a + b s) + c (c0 = (e0 + v pk0) + m), limbs < lvl.
-enum { EW_ADD = 0, EW_SUB = 1, EW_NEG = 2, EW_COPY = 3, EW_DEC = 4, EW_ENC0 = 5 };
+// to every element (limb, k) by one launch.  Op: out = a + b, a - b, -a, a, or
+// a + b s (decryption: a = c0, b = c1, s = the secret key), limbs < lvl.
+enum { EW_ADD = 0, EW_SUB = 1, EW_NEG = 2, EW_COPY = 3, EW_DEC = 4 };
 struct EwOp {
   uint64_t *out;
-  const uint64_t *a, *b, *s, *c;
+  const uint64_t *a, *b, *s;
   uint32_t kind, lvl;
 };
 struct EwProg {

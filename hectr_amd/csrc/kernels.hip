@@ -999,9 +999,6 @@ __global__ void ew_prog_kernel(EwProg pr, unsigned logn, const ModConst *mc)
     case EW_DEC:
       r = add_mod(x, mul_mod(o.b[off], o.s[off], m), m.q);
       break;
-    case EW_ENC0:
-      r = add_mod(add_mod(x, mul_mod(o.b[off], o.s[off], m), m.q), o.c[off], m.q);
-      break;
     default:
       r = x;
     }
