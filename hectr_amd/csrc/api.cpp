@@ -880,8 +880,8 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
   if (G.init && defer_ok(0) && slots && !(slots & (slots - 1)) && slots <= GPQHE_DCD_ONEPASS &&
       slots <= G.n / 2 && !(pt->flags & GPQHE_F_COEFF) && pt->nlimbs >= 1 && pt->nlimbs <= 2) {
     // the small-N step's tail: the queued elementwise program (he_add, he_neg,
-    // he_copy_ct, he_add, he_dec), the inverse transform and the decoder in
-    // one launch (k_ew_decode)
+    // he_copy_ct, he_add, he_dec), then the inverse transform and the decoder
+    // in one more launch (k_ew_decode)
     if (!g_pgemv.empty())
       flush_gemvs();
     if (!g_pecd.empty() || !g_penc.empty())
