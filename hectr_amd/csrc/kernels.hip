@@ -2533,7 +2533,10 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
     rows8_inv<LOGN2>(r, lds, ar, n1 + row0);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      yo[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+      // streaming store: the batch's row-pass output (256 pairs: 1 GiB) is read
+      // back from HBM by ks_cols4 anyway (d2_rows 649 -> 641 us, 40.4k ->
+      // 40.6k ct-mult/s, same box)
+      __builtin_nontemporal_store(ar.canon(r[k]), &yo[(row << LOGN2) + l + T::TA * k]);
   });
 }
 
