@@ -2223,7 +2223,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        (out + (size_t)k * n2)[vo] = ar.store_lazy(r[k]);  // T1 / conv: read lazily by the row passes
+        __builtin_nontemporal_store(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }
@@ -3250,7 +3250,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        (out + (size_t)k * n2)[vo] = ar.store_lazy(r[k]);  // T1 / conv: read lazily by the row passes
+        __builtin_nontemporal_store(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }
