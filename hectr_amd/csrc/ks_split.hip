@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           }
           ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + 8 * th);
 #pragma unroll
-          for (int i = 0; i < 4; i++)
+          for (int i = 0; i < 4; i++)  // (non-temporal stores here: 1840 -> 2245 us per chunk)
             d2[i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
         }
       } else {
