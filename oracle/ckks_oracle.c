@@ -26,7 +26,7 @@
  * NTT / CRT / key-switch identities (tests/ckks_model.py), and (b) end to
  * end against the reference's own committed encrypted run
  * tests/results/cstr-hempc.bin and plaintext run cstr-mpc.bin (written at
- * reference tests/hectr.c:751-756,812-817) through tests/cstr_loop.py.
+ * reference tests/hectr.c:751-756,812-817) through hectr_amd/cstr.py.
  *
  * Every algorithmic choice that affects output bits (prime selection, root
  * choice, NTT ordering, RNG streams, fast basis conversion, rounding in

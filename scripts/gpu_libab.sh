@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU parity tests on the working tree's library, then the bench alternating
-# between a baseline library (hectr_amd/lib_base, built from another commit)
+# between a baseline library (hectr_amd/lib_ab, built from another commit; delete it after the A/B: it is not gpurun-ignored)
 # and the working tree's, ROUNDS times each, same box.
 #   RUN=name [TESTS="tests/..."] bash scripts/gpu_libab.sh
 set -o pipefail
@@ -15,7 +15,7 @@ if [ -z "$NO_TESTS" ]; then
 fi
 B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr ${LEGS:---no-ntt} --alt-bits 0 ${BENCH_ARGS}"
 for r in $(seq 1 ${ROUNDS:-2}); do
-  GPQHE_LIB=hectr_amd/lib_base/libgpqhe.so timeout -k 10 300 $B > $OUT/bench_base_$r.log 2>&1 || exit 1
+  GPQHE_LIB=hectr_amd/lib_ab/libgpqhe.so timeout -k 10 300 $B > $OUT/bench_base_$r.log 2>&1 || exit 1
   timeout -k 10 300 $B > $OUT/bench_new_$r.log 2>&1 || exit 1
   # VARIANTS="name=ENVVAR=VALUE ...": the working tree's library under env switches
   for v in ${VARIANTS}; do

@@ -175,6 +175,36 @@ def test_ntt_batch_bitexact(oracle, product, name, npolys):
     assert np.array_equal(host, orig)
 
 
+@pytest.mark.parametrize("name,npolys", [("bench51", 1024), ("bench", 97)])
+def test_ntt_batch_full_shape(oracle, product, name, npolys):
+    """Config 2 at its full shape (1024 polys x 8 limbs at
+    N=2^16, the bench's prime set) and 97 polys on the 60-bit set: ntt_batch
+    runs the batch in groups of 48 polys (api.cpp ntt_batch), so these cover
+    every group offset, the row pass's member split at a full group and a
+    partial last group (97 = 48 + 48 + 1).  Forward and inverse are each
+    compared residue by residue with the oracle, not only the roundtrip."""
+    import torch
+    init_both(oracle, product, name)
+    n, L = product.n, product.L
+    host = np.zeros(npolys * L * n, dtype=np.uint64)
+    oracle.lib.poly_fill_uniform(host.ctypes.data, npolys, L, 0x48454354520001)
+    dev = torch.empty(npolys * L * n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.poly_fill_uniform(dev.data_ptr(), npolys, L, 0x48454354520001)
+    product.sync()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    for fwd in (True, False):
+        fn = "poly_ntt_batch" if fwd else "poly_intt_batch"
+        getattr(oracle.lib, fn)(host.ctypes.data, npolys, L)
+        getattr(product.lib, fn)(dev.data_ptr(), npolys, L)
+        product.sync()
+        got = dev.cpu().numpy().view(np.uint64)
+        bad = np.flatnonzero(got != host)
+        assert bad.size == 0, f"{fn}: {bad.size} residues differ, first at poly {bad[0] // (L * n)}"
+        del got
+    del host, dev
+
+
 def mul_batch_both(oracle, product, name, cnt, lvl=None, seeds=(1, 2)):
     """he_mul_rescale_batch of `cnt` random-residue pairs at level `lvl` on
     both engines (same keys, same inputs); returns (oracle, product) outputs."""
@@ -217,7 +247,7 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
 
 @pytest.mark.parametrize("name,cnt,chunk", [("bench51", 17, None), ("bench51", 24, None), ("bench_d2", 17, None),
                                             ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None),
-                                            ("c5", 17, None), ("c15", 17, None)])
+                                            ("c5", 17, None), ("c5", 64, None), ("c15", 17, None)])
 def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
     """The headline shape (bench.py): n=2^16, L=8,
     dnum=2, K=4 on 17 and 24 pairs (the split key switch's pair ranges of
@@ -227,8 +257,9 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     loop, a short last chunk) and the bench's own 256 pairs (two 128-pair
     chunks of the 8 GiB workspace, about 3 pairs per quarter), every output
     residue compared with the oracle.  Also 17 pairs of config 5 (n=2^17, L=12,
-    the three-digit split key switch) and of c15 (integer moduli: two pair
-    streams per workgroup)."""
+    the three-digit split key switch), config 5's own bench shape (64 pairs per
+    GPU, bench.py's c5 leg: its pair ranges and member split) and 17 of c15
+    (integer moduli: two pair streams per workgroup)."""
     if chunk:
         monkeypatch.setenv("GPQHE_CHUNK", str(chunk))
     want, got = mul_batch_both(oracle, product, name, cnt, seeds=(21, 22))
