@@ -350,7 +350,37 @@ def cstr_c_caller(reps=3):
     pmed = sorted(plain)[len(plain) // 2] if plain else None
     return {"steps": 40, "closed_loop_ms_median": med, "steps_per_s": 40e3 / med, "runs_ms": ms,
             "plaintext_closed_loop_ms_median": pmed,
-            "encrypted_regulator_ms_per_step": (med - pmed) / 40 if pmed is not None else None}
+            "encrypted_regulator_ms_per_step": (med - pmed) / 40 if pmed is not None else None,
+            "config4_c_driver": cstr_c_driver(reps)}
+
+
+def cstr_c_driver(reps=3, steps=100):
+    """Config 4 at its own shape: the reference's unchanged hectr_simulate
+    with N = 100 (horizon 10, 32 slots) through harness/cstr_run.c on the
+    product library; steps/s from the closed-loop time the reference's own
+    TEST_DO/TEST_DONE prints (keygen excluded, timed separately by it)."""
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "_ref", "cstr-run")
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "hectr_amd", "lib"), GPQHE_SEED="5")
+    ms, keygen = [], None
+    for _ in range(reps):
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([exe, "hempc", str(steps), os.path.join(d, "t.bin")], env=env, capture_output=True,
+                               text=True, timeout=120)
+            log = r.stdout + r.stderr
+            m = re.search(r"closed-loop simulate\s+([0-9.]+) ms", log)
+            if r.returncode or not m:
+                return {"error": log[-300:]}
+            ms.append(float(m.group(1)))
+            k = re.search(r"he_genrk\s+([0-9.]+) ms", log)
+            keygen = float(k.group(1)) if k else None
+    med = sorted(ms)[len(ms) // 2]
+    return {"steps": steps, "horizon": steps // 10, "slots": 32, "closed_loop_ms_median": med,
+            "steps_per_s": steps * 1e3 / med, "runs_ms": ms, "genrk_ms": keygen,
+            "note": "reference hectr_simulate unchanged; parity: tests/test_gpu_hectr_caller.py (bit-equal to the "
+                    "oracle), tests/test_cstr_driver.py (fixture cstr-mpc-100.bin)"}
 
 
 def usable_cpus():

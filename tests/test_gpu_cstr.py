@@ -5,10 +5,9 @@ tests/hectr.c:760-819) driven through the MI355X product library.
   decoded trajectory within 1e-9 relative of the reference's committed
   encrypted run cstr-hempc.bin and of cstr-mpc.bin, and -- same seed --
   bit-identical to the oracle-driven loop (the u values are equal doubles).
-* config 4 shape: 100 steps (horizon 10, 32 slots) against the plaintext
-  restatement of ctr_simulate at the same N (no committed fixture exists for
-  N = 100; the restatement is pinned by the N = 40 fixture in
-  tests/test_cstr_fixtures.py).
+* config 4 shape: 100 steps (horizon 10, 32 slots) against the reference's
+  own plaintext ctr_simulate at N = 100 (tests/golden/cstr-mpc-100.bin,
+  tests/make_cstr_fixture.sh) and the restatement's plaintext loop.
 """
 import os
 
@@ -57,3 +56,5 @@ def test_cstr_100_steps_on_gpu(product):
     x, u = pb.simulate(reg)
     reg.close()
     assert rel(x, xp) < 1e-8 and rel(u, up) < 1e-8
+    rec, ref = pb.records(x, u), load("cstr-mpc-100")
+    assert rel(rec["x"], ref["x"]) < 1e-6 and rel(rec["u"], ref["u"]) < 1e-6
