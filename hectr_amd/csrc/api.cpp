@@ -886,10 +886,14 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
       flush_gemvs();
     if (!g_pecd.empty() || !g_penc.empty())
       flush_pending();
+    // workspace and pinned buffer first: the pool's out-of-memory path flushes
+    // the elementwise queue, which must still hold the program then (its ops
+    // may name freed blocks the flush would otherwise release under it)
+    Ws c((size_t)pt->nlimbs << G.logn);
+    double *zd = (double *)zpin(zb);
     const EwProg p = g_pew;
     g_pew.count = 0;
-    Ws c((size_t)pt->nlimbs << G.logn);
-    k_ew_decode(p, (double *)zpin(zb), pt->data, pt->nlimbs, slots, pt->scale, c.p);
+    k_ew_decode(p, zd, pt->data, pt->nlimbs, slots, pt->scale, c.p);
     HIP_CHECK(hipStreamSynchronize(G.stream));
     memcpy(z, g_zpin, zb);
     return;

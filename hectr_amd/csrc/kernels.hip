@@ -2223,7 +2223,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        __builtin_nontemporal_store(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
+        ST_STREAM(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }
@@ -2536,7 +2536,7 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
       // streaming store: the batch's row-pass output (256 pairs: 1 GiB) is read
       // back from HBM by ks_cols4 anyway (d2_rows 649 -> 641 us, 40.4k ->
       // 40.6k ct-mult/s, same box)
-      __builtin_nontemporal_store(ar.canon(r[k]), &yo[(row << LOGN2) + l + T::TA * k]);
+      ST_STREAM(ar.canon(r[k]), &yo[(row << LOGN2) + l + T::TA * k]);
   });
 }
 
@@ -3250,7 +3250,7 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
       ar.template fwd<4>(r, T + 16 * g, 3);
 #pragma unroll
       for (int k = 0; k < 16; k++)
-        __builtin_nontemporal_store(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
+        ST_STREAM(ar.store_lazy(r[k]), &(out + (size_t)k * n2)[vo]);  // T1 / conv: read lazily by the row passes
     });
     (void)q2;
   }

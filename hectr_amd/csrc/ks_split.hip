@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           uint64_t *o = dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff;
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            __builtin_nontemporal_store(ar.canon(r[k]), &o[(row << LOGN2) + l + T::TA * k]);
+            ST_STREAM(ar.canon(r[k]), &o[(row << LOGN2) + l + T::TA * k]);
         }
       }
     }

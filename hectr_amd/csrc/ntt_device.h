@@ -273,6 +273,14 @@ __device__ __forceinline__ double fbc_term(double y, double c, double cq, double
   return f64_mulmod(y, c, cq, q);
 }
 
+// Streaming stores for the pipeline intermediates (read back once by the next
+// kernel); GPQHE_PLAIN_STORES builds the plain-store variant for A/B runs.
+#ifdef GPQHE_PLAIN_STORES
+#define ST_STREAM(v, p) (*(p) = (v))
+#else
+#define ST_STREAM(v, p) __builtin_nontemporal_store((v), (p))
+#endif
+
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
 constexpr uint64_t F64_LAZY = 1ull << 50;  // and its lazy stage reduction below this
 

@@ -26,7 +26,10 @@ def init(backend: str):
         if backend == "nccl":
             import torch
             kw["device_id"] = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-        dist.init_process_group(backend, **kw)
+        import datetime
+        # bounded rendezvous / collectives: a rank that never arrives ends the
+        # job instead of hanging it (bench.py's launcher also polls its ranks)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=300), **kw)
     return rank, world, local
 
 

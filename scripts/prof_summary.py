@@ -48,7 +48,7 @@ def summarise(run, prefix):
     for r in csv.DictReader(open(os.path.join(run, prefix + "kt", prefix + "kt_kernel_trace.csv"))):
         dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     pmc = {}
-    for f in ("fetch", "write", "hit", "sq"):
+    for f in ("fetch", "write", "hit", "sq", "f64"):
         d = prefix + f
         for k, cs in counters(os.path.join(run, d, d + "_counter_collection.csv")).items():
             for c, v in cs.items():
@@ -74,6 +74,14 @@ def summarise(run, prefix):
         if c.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in c:
             e["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / (c["GRBM_GUI_ACTIVE"] / XCDS)
             e["clock_GHz"] = c["GRBM_GUI_ACTIVE"] / XCDS / (e["mean_us"] * 1e3)
+            # VALU issue fraction from the instruction count: every FP64 VALU
+            # instruction of a wave64 holds the SIMD-32's FP64 pipe 4 cycles
+            # (78.6 TF = 256 CUs x 4 SIMDs x 16 FMA lanes x 2 x 2.4 GHz)
+            e["valu_frac"] = c["SQ_INSTS_VALU"] * 4 / SIMDS / (c["GRBM_GUI_ACTIVE"] / XCDS)
+        f64 = [c.get("SQ_INSTS_VALU_" + x) for x in ("FMA_F64", "MUL_F64", "ADD_F64", "TRANS_F64")]
+        if all(v is not None for v in f64):
+            e["valu_mix"] = {k.lower(): c["SQ_INSTS_VALU_" + k] for k in
+                             ("FMA_F64", "MUL_F64", "ADD_F64", "TRANS_F64", "INT32", "INT64", "CVT") if "SQ_INSTS_VALU_" + k in c}
         for q in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_BUSY_CYCLES"):
             if q in c:
                 e[q.lower()] = c[q]
@@ -84,7 +92,9 @@ def summarise(run, prefix):
 def main(run, tag):
     os.makedirs(os.path.dirname(tag) or ".", exist_ok=True)
     meta = {"source": run, "fetch_correction": "x2 (gfx950 FETCH_SIZE halves wide reads)",
-            "units": "bytes per launch", "valu_busy": "SQ_ACTIVE_INST_VALU*4/1024/(GRBM_GUI_ACTIVE/8)"}
+            "units": "bytes per launch", "valu_busy": "SQ_ACTIVE_INST_VALU*4/1024/(GRBM_GUI_ACTIVE/8)",
+            "valu_frac": "SQ_INSTS_VALU*4/1024/(GRBM_GUI_ACTIVE/8) (4 cycles per wave64 FP64 instruction)",
+            "mean_us": "kernel trace of a bench run with the bench's own --steps 10 --warmup 2"}
     full = os.path.join(run, "bench_full.log")
     if os.path.exists(full):
         lines = [l for l in open(full) if l.startswith('{"metric"')]
