@@ -373,12 +373,13 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 // (launch bound: two workgroups per CU; the inverse then spills 16 VGPRs
 // but the roundtrip runs 7.55 -> 7.45 ms, same box; the inverse alone at one
 // workgroup per CU, no spills, ran 7.39 -> 7.50 ms)
-template <int LOGN2, bool INV, int QN>
-__global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+template <int LOGN2, bool INV, int QN, bool W8 = false, int MINW = 2 * QN>
+__global__ void __launch_bounds__(256 * QN, MINW) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                              const ModConst *mcs, unsigned members)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];
+  // (integer moduli stage 16-byte forward entries whatever W8 says)
   __shared__ __attribute__((aligned(16))) uint64_t rtw[2 * RowTw<LOGN2>::ENTRIES];
   const unsigned n1 = 1u << (logn - LOGN2), tiles = n1 / T::R, per = s.per, polys = s.count / per;
   unsigned grp, mi;  // group = (slot, tile); members = poly ranges
@@ -403,12 +404,16 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
     using A0 = std::decay_t<decltype(ar0)>;
     constexpr bool F = std::is_same<A0, ArF64>::value;
     // FP64: (w, w/q) of this direction; integer: the forward (w, w') pairs
-    RowTw<LOGN2>::stage(rtw, INV && F ? (const uint64_t *)ar0.itw : (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x,
-                        256 * QN);
+    if constexpr (W8 && F)
+      RowTw<LOGN2>::template stage<true>(rtw, INV ? (const uint64_t *)ar0.itw : (const uint64_t *)ar0.tw, n1 + row0,
+                                         threadIdx.x, 256 * QN);
+    else
+      RowTw<LOGN2>::stage(rtw, INV && F ? (const uint64_t *)ar0.itw : (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x,
+                          256 * QN);
     __syncthreads();
     const auto ar = [&] {
       if constexpr (F)
-        return row_policy<LOGN2, false>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0), INV ? rtw : nullptr);
+        return row_policy<LOGN2, W8>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0), INV ? rtw : nullptr);
       else
         return row_policy<LOGN2, false>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0));
     }();
@@ -441,7 +446,21 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
     constexpr int QN = 2;
     const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
-    if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
+    static const int var = getenv("GPQHE_NTT_INV_VARIANT") ? atoi(getenv("GPQHE_NTT_INV_VARIANT")) : 2;  // A/B (temporary)
+    if (polys >= 4 * QN && in.per == out.per && inv && var == 1) {
+      const unsigned members = std::max(1u, polys / (4 * 3));
+      hipLaunchKernelGGL((ntt_rows_q_kernel<LOGN2, true, 3, false, 3>), dim3(xcd_blocks(members, groups)), dim3(768), 0,
+                         G.stream, in, out, logn, tw, G.dev.mc, members);
+    } else if (polys >= 4 * QN && in.per == out.per && inv && var == 2) {
+      const unsigned members = std::max(1u, polys / (4 * QN));
+      hipLaunchKernelGGL((ntt_rows_q_kernel<LOGN2, true, QN, true>), dim3(xcd_blocks(members, groups)), dim3(256 * QN),
+                         0, G.stream, in, out, logn, tw, G.dev.mc, members);
+    } else if (polys >= 4 * QN && in.per == out.per && var == 3) {
+      const unsigned members = std::max(1u, polys / (4 * QN));
+      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true> : ntt_rows_q_kernel<LOGN2, false, QN, true>;
+      hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
+                         G.dev.mc, members);
+    } else if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
       const unsigned members = std::max(1u, polys / (4 * QN));  // ~4 polys per quarter
       auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN> : ntt_rows_q_kernel<LOGN2, false, QN>;
       hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
@@ -2118,7 +2137,6 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
         return;
       }
       const unsigned mi_ = lo + i;
-      const uint64_t w = tab.ysc[2 * mi_], wp = tab.ysc[2 * mi_ + 1];
       const uint64_t *src = yb + ((size_t)i << logn);
       if (i)
         __syncthreads();
@@ -2148,7 +2166,7 @@ __global__ void __launch_bounds__(256, 2) ks_cols4_kernel(const uint64_t *ybuf, 
           ar.template inv<LEA>(r, T, 4);
 #pragma unroll
           for (int k = 0; k < EA; k++)
-            y[it][i][k] = F64 ? ar.mulc_d(r[k], w, wp) : ar.mulc(r[k], w, wp);
+            y[it][i][k] = F64 ? ar.canon_d(r[k]) : ar.canon(r[k]);  // (scaled by d2_rows)
         }
       });
     };
@@ -2334,8 +2352,8 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           const double wb = (double)eb[256 * k], wa = (double)ea[256 * k];
-          const double tb = f64_mulmod(r[k], wb, wb * ar.qinv, ar.q);
-          const double ta = f64_mulmod(r[k], wa, wa * ar.qinv, ar.q);
+          const double tb = f64_mulmod_h(r[k], wb, ar.q, ar.qinv);
+          const double ta = f64_mulmod_h(r[k], wa, ar.q, ar.qinv);
           f0[k] = j ? f0[k] + tb : tb;
           f1[k] = j ? f1[k] + ta : ta;
           if (fold) {
@@ -2478,11 +2496,14 @@ static void ks_fused_launch(const uint64_t *y, uint64_t *T1, const uint64_t *d2n
 // and its inverse row pass (the column pass completes the INTT); replaces the
 // tensor kernel and the separate row pass (d0, d1 are formed by their
 // consumers, D01Src).
+// ysc (split key switch with the INTT's column pass in ks_cols4): the ModUp
+// factor n^-1 [(Qj/q_i)^-1]_{q_i} per limb is applied here, where the kernel
+// waits on HBM with VALU to spare, instead of in the VALU-bound ks_cols4.
 template <int LOGN2>
 __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y, const uint64_t *a,
                                                        const uint64_t *b, size_t in_stride, size_t in_pstride,
                                                        unsigned logn, unsigned lvl, unsigned count, Tw2 tw,
-                                                       const ModConst *mcs)
+                                                       const ModConst *mcs, const uint64_t *ysc)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t lds[T::WORDS];
@@ -2516,12 +2537,18 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
         // exact FP64 product of canonical residues, |.| < 1.5 q (a valid
         // inverse-pass input); canonical only for the optional d2 copy
         const double bb = f64_from_u52(B1[k]);
-        r[k] = f64_mulmod(f64_from_u52(A1[k]), bb, bb * ar.qinv, ar.q);
+        r[k] = f64_mulmod_h(f64_from_u52(A1[k]), bb, ar.q, ar.qinv);
         if (d2)
           raw[k] = ar.canon(r[k]);
+        if (ysc) {
+          // times s: |r| <= q/2 after the reduction, so with the recomputed
+          // s / q the quotient is off by < 1/2 + 0.75 q 2^-52: |r s - .| < 0.9 q
+          const double sd = f64_from_u52(ysc[2 * limb]);
+          r[k] = f64_mulmod_h(f64_red(r[k], ar.q, ar.qinv), sd, ar.q, ar.qinv);
+        }
       } else {
         raw[k] = mul_mod(A1[k], B1[k], mc);
-        r[k] = A::load(raw[k]);
+        r[k] = A::load(ysc ? mul_shoup(raw[k], ysc[2 * limb], ysc[2 * limb + 1], mc.q) : raw[k]);
       }
     }
     if (d2) {  // the NTT-form copy for the streaming ks_rows (the split key switch forms it from a, b)
@@ -2557,7 +2584,8 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
     // reads a1, b1; writes its inverse row pass (and d2 when asked)
     ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * (d2 ? 4 : 3));
     hipLaunchKernelGGL((d2_rows_kernel<LOGN2>), dim3(lvl * count * (n / 2048)), dim3(256), 0, G.stream, d2, ybuf, a,
-                       b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc);
+                       b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc,
+                       cols ? (const uint64_t *)nullptr : (const uint64_t *)tab.ysc);
   }
   if (!cols)  // the column pass runs inside ks_cols4 (invc)
     return;
@@ -2641,6 +2669,15 @@ struct DownTable {
   uint64_t *c;       // [nd][keep]  [Dprod/d]_t
   uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
   double *cd;        // [nd][keep][2] ([Dprod/d]_t, that / q_t) as doubles (FP64 conversion)
+  // Split key switch (mul_split_launch): the ModDown's constant factors folded
+  // into the relinearization key (ksq kernels, per basis slot) and into the
+  // conversion constants, so no kernel multiplies by them:
+  //   kept slot t:    key x [Dprod^-1]_t; conversion [Dprod/d]_t [Dprod^-1]_t = [d^-1]_t
+  //   dropped slot t: key x n^-1 [(Dprod/d)^-1]_d (the INTT's scale, ysc)
+  uint64_t *ksc;     // [nm]        key scale s_t
+  uint64_t *kps;     // [nm][2]     [P s_t]_t + Shoup (the P (d0, d1) term of q slots)
+  uint64_t *cf;      // [nd][keep]  [d^-1]_t (Montgomery form)
+  double *cdf;       // [nd][keep][2] ([d^-1]_t, that / q_t)
   unsigned keep, nd;
   int f64;           // every modulus < 2^51 (and FP64 enabled): FP64 conversion
 };
@@ -2698,9 +2735,34 @@ static DownTable &down_table(unsigned lvl, int mode)
     ysc[2 * d] = w;
     ysc[2 * d + 1] = (uint64_t)(((unsigned __int128)w << 64) / G.q[md]);
   }
+  // folded factors of the split key switch (see DownTable)
+  std::vector<uint64_t> ksc(nm), kps(2 * (size_t)nm), cf((size_t)nd * keep);
+  std::vector<double> cdf((size_t)nd * keep * 2);
+  for (unsigned t = 0; t < nm; t++) {
+    const unsigned m = mods[t];
+    ksc[t] = t < keep ? dinv[t] : ysc[2 * (t - keep)];
+    kps[2 * t] = hm_mul_mod(G.mc[m].pmod, ksc[t], G.q[m]);
+    kps[2 * t + 1] = (uint64_t)(((unsigned __int128)kps[2 * t] << 64) / G.q[m]);
+  }
+  for (unsigned d = 0; d < nd; d++)
+    for (unsigned t = 0; t < keep; t++) {
+      const uint64_t qt = G.q[mods[t]];
+      const uint64_t di = hm_inv_mod(G.q[mods[keep + d]] % qt, qt);
+      cf[(size_t)d * keep + t] = hm_mul_mod(di, G.mc[mods[t]].r64, qt);  // Montgomery form
+      cdf[2 * ((size_t)d * keep + t)] = (double)di;
+      cdf[2 * ((size_t)d * keep + t) + 1] = (double)di / (double)qt;
+    }
   DownTable tab;
   tab.keep = keep;
   tab.nd = nd;
+  auto up = [](auto *&dst, const auto &v) {
+    HIP_CHECK(hipMalloc(&dst, v.size() * 8));
+    HIP_CHECK(hipMemcpy(dst, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+  };
+  up(tab.ksc, ksc);
+  up(tab.kps, kps);
+  up(tab.cf, cf);
+  up(tab.cdf, cdf);
   tab.f64 = G.twd != nullptr;
   for (unsigned t = 0; t < nm; t++)
     tab.f64 &= G.q[mods[t]] < (1ull << 51);
@@ -3098,7 +3160,11 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
 // The converted polynomial never reaches HBM in coefficient form and the
 // combine is the row pass's epilogue.
 // ===========================================================================
-template <int LOGT, int NT, bool X5, bool F64>
+// PRE (split key switch): the drop limbs arrive already scaled by
+// n^-1 [(Dprod/d)^-1]_d (folded into the key) and conv takes the folded
+// constants [d^-1]_t (conv x [Dprod^-1]_t: the kept slots' epilogue has no
+// multiply); else the scaling runs here and conv uses [Dprod/d]_t.
+template <int LOGT, int NT, bool X5, bool F64, bool PRE = false>
 __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size_t x_pstride, size_t x_off, uint64_t *conv,
                                                           unsigned logn, unsigned lvl, unsigned L, unsigned members,
                                                           unsigned ngroups, DownTable tab, Tw2 tw,
@@ -3159,7 +3225,9 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
         ar.template inv<LEA>(r, T, 4);
 #pragma unroll
         for (int k = 0; k < EA; k++) {
-          const uint64_t v = F64 ? ar.mulc_d(r[k], w, wp) : ar.mulc(r[k], w, wp);
+          // FP64 conversion: canonical doubles; integer sums: canonical words
+          const uint64_t v = PRE ? (F64 ? ar.canon_d(r[k]) : ar.canon(r[k]))
+                                 : (F64 ? ar.mulc_d(r[k], w, wp) : ar.mulc(r[k], w, wp));
           if (d < 4)
             y[it][d < 4 ? d : 0][k] = v;
           else if constexpr (X5)
@@ -3184,10 +3252,12 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
     const unsigned m = basis_mod(t, lvl, L);
     const ModConst mc = mcs[m];
     const uint64_t q = mc.q, q2 = 2 * q;
+    const uint64_t *ctab = PRE ? tab.cf : tab.c;
+    const double *cdtab = PRE ? tab.cdf : tab.cd;
     uint64_t cc[5];
 #pragma unroll
     for (int d = 0; d < 5; d++)
-      cc[d] = d < (int)nd ? tab.c[(size_t)d * keep + t] : 0;
+      cc[d] = d < (int)nd ? ctab[(size_t)d * keep + t] : 0;
     if (u)
       __syncthreads();  // the previous target's round B has read the tile
     uint64_t *out = conv + (((size_t)p * keep + t) << logn) + (size_t)tile * C;
@@ -3205,8 +3275,8 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
             double cw[5], cq[5];
 #pragma unroll
             for (int d = 0; d < 5; d++) {
-              cw[d] = d < (int)nd ? tab.cd[2 * ((size_t)d * keep + t)] : 0.0;
-              cq[d] = d < (int)nd ? tab.cd[2 * ((size_t)d * keep + t) + 1] : 0.0;
+              cw[d] = d < (int)nd ? cdtab[2 * ((size_t)d * keep + t)] : 0.0;
+              cq[d] = d < (int)nd ? cdtab[2 * ((size_t)d * keep + t) + 1] : 0.0;
             }
 #pragma unroll
             for (int k = 0; k < EA; k++) {
@@ -3320,7 +3390,7 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
 // limbs of poly p sit at X + p x_pstride + x_off (inverse row pass done)
 template <int LOGT1>
 static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, size_t x_off, unsigned npoly,
-                          unsigned lvl, const DownTable &tab)
+                          unsigned lvl, const DownTable &tab, bool pre)
 {
   const unsigned n = G.n, keep = tab.keep, tiles = n / 4096;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
@@ -3335,10 +3405,17 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
       hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, X, x_pstride, x_off,
                          conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     };
-    if (tab.f64 && FBC64_DN)
+    if (pre) {
+      if (tab.f64 && FBC64_DN)
+        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true, true>) : go(dn_cols_kernel<LOGT1, NT, true, true, true>);
+      else
+        tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false, true>)
+                    : go(dn_cols_kernel<LOGT1, NT, true, false, true>);
+    } else if (tab.f64 && FBC64_DN) {
       tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true>) : go(dn_cols_kernel<LOGT1, NT, true, true>);
-    else
+    } else {
       tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false>) : go(dn_cols_kernel<LOGT1, NT, true, false>);
+    }
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -3349,7 +3426,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
 {
   const unsigned n = G.n, keep = tab.keep;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
-  dn_cols_stage<LOGT1>(conv, X, x_pstride, (size_t)keep << G.logn, npoly, lvl, tab);
+  dn_cols_stage<LOGT1>(conv, X, x_pstride, (size_t)keep << G.logn, npoly, lvl, tab, false);
   // reads conv and X, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 3.0);
   hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
@@ -3429,15 +3506,15 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
     // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per
     // workgroup; writes the inverse row pass of the nd dropped slots
     ProfScope ps(KC_KSQ_DROP, 8.0 * n * count * ((double)ndig * nd + 2.0 * nd + (rescale ? 4.0 - 1.0 : 0.0)));
-    ksq_run(LOGN2, ndig, allf, false, T1, d01, evkm, accd, (size_t)nd * n, nullptr, dn.dinv, dn.dinvp, count, lvl,
+    ksq_run(LOGN2, ndig, allf, false, T1, d01, evkm, accd, (size_t)nd * n, nullptr, dn.ksc, dn.kps, count, lvl,
             nm, keep, nd);
   }
-  dn_cols_stage<LOGT1>(conv, accd, (size_t)nd * n, 0, 2 * count, lvl, dn);
+  dn_cols_stage<LOGT1>(conv, accd, (size_t)nd * n, 0, 2 * count, lvl, dn, true);
   {
     // reads T1 (ndig - 1 converted limbs), the four input limbs and the two
     // conv limbs per pair and kept slot; writes the two output limbs
     ProfScope ps(KC_KSQ_KEEP, 8.0 * n * count * keep * ((double)ndig - 1.0 + 4.0 + 2.0 + 2.0));
-    ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.dinv, dn.dinvp, count, lvl, nm, 0,
+    ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.ksc, dn.kps, count, lvl, nm, 0,
             keep);
   }
   if (own)

@@ -26,6 +26,10 @@
 //   KEEP = true (t < drop_lo): the ModDown epilogue follows at once, so the
 //     accumulators never reach HBM: out = (f - NTTrows(conv)) D^-1 with conv
 //     from dn_cols (the key switch of the dropped limbs ran first).
+// The ModDown's constant factors are folded in (DownTable ksc / kps): the key
+// tile is scaled by s_t as it is staged (kept slots: D^-1, so f arrives as
+// f D^-1 and conv as conv D^-1 from dn_cols' folded constants; dropped slots:
+// the INTT's n^-1 [(D/d)^-1]_d), and P (d0, d1) by [P s_t]_t.
 // Inputs a, b are read here and by d2_rows only; out may alias them when each
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
@@ -33,7 +37,7 @@
 template <int LOGN2, int NDIG, int QN, bool ALLF, bool KEEP, bool LTW>
 __global__ void __launch_bounds__(256 * QN, 1)
     ksq_kernel(const uint64_t *T1, size_t t1_stride, D01Src d01, const uint64_t *evkm, uint64_t *dst,
-               size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp, unsigned logn,
+               size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned logn,
                unsigned lvl, unsigned L, unsigned nm, unsigned nmod, unsigned alpha, unsigned count, unsigned members,
                unsigned t_lo, unsigned t_n, Tw2 tw, const ModConst *mcs)
 {
@@ -61,9 +65,11 @@ __global__ void __launch_bounds__(256 * QN, 1)
   const unsigned row0 = tile * T::R;
   const size_t toff = (size_t)row0 << LOGN2;
   const bool f64 = ALLF || (q < F64_QMAX && tw.fwdd);  // key words as plain doubles (to_mont_kernel)
+  const uint64_t sk = ksc[t];  // the folded ModDown factor of this slot
   for (unsigned idx = threadIdx.x; idx < 2 * NDIG * 2048; idx += 256 * QN) {
     const unsigned c = idx >> 11, w = idx & 2047;
-    const uint64_t e = evkm[(((size_t)c * nmod + m) << logn) + toff + w];
+    // plain (FP64 moduli) or Montgomery form: either way x s_t stays in its form
+    const uint64_t e = mul_mod(evkm[(((size_t)c * nmod + m) << logn) + toff + w], sk, mc);
     kl[c][w] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
   }
   __syncthreads();
@@ -177,8 +183,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
           for (int k = 0; k < 8; k++) {
             const double eb = __longlong_as_double((long long)kl[2 * j][256 * k + th]);
             const double ea = __longlong_as_double((long long)kl[2 * j + 1][256 * k + th]);
-            const double tb = f64_mulmod(r[k], eb, eb * ar.qinv, ar.q);
-            const double ta = f64_mulmod(r[k], ea, ea * ar.qinv, ar.q);
+            const double tb = f64_mulmod_h(r[k], eb, ar.q, ar.qinv);
+            const double ta = f64_mulmod_h(r[k], ea, ar.q, ar.qinv);
             f0[k] = u ? f0[k] + tb : tb;
             f1[k] = u ? f1[k] + ta : ta;
             if (u == 1) {  // two products (< 3 q): fold before the next term
@@ -201,7 +207,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
         // q limb: own digit x = a1 b1 (the NTT-form d2 limb) and P (d0, d1),
         // from the four input words at this thread's natural positions 8 th + k
         if constexpr (F) {
-          const double Pd = f64_from_u52(mc.pmod), Pq = Pd * ar.qinv;
+          const double Pd = f64_from_u52(kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             if (h || !EARLY)
@@ -213,13 +219,13 @@ __global__ void __launch_bounds__(256 * QN, 1)
               const double A1 = f64_from_u52(inw[2][e]), B1 = f64_from_u52(inw[3][e]);
               const double eb = __longlong_as_double((long long)kl[2 * jo][256 * k + th]);
               const double ea = __longlong_as_double((long long)kl[2 * jo + 1][256 * k + th]);
-              const double x = f64_mulmod(A1, B1, B1 * ar.qinv, ar.q);  // |x| < 1.5 q
-              const double d0 = f64_mulmod(A0, B0, B0 * ar.qinv, ar.q);
-              const double d1 = f64_red(f64_mulmod(A0, B1, B1 * ar.qinv, ar.q) + f64_mulmod(A1, B0, B0 * ar.qinv, ar.q),
+              const double x = f64_mulmod_h(A1, B1, ar.q, ar.qinv);  // |x| < 1.5 q
+              const double d0 = f64_mulmod_h(A0, B0, ar.q, ar.qinv);
+              const double d1 = f64_red(f64_mulmod_h(A0, B1, ar.q, ar.qinv) + f64_mulmod_h(A1, B0, ar.q, ar.qinv),
                                         ar.q, ar.qinv);
               // |f| <= q/2 + 1.5 q after the fold, then + two products < 1.5 q
-              const double g0 = f64_red(f0[k], ar.q, ar.qinv) + f64_mulmod(x, eb, eb * ar.qinv, ar.q);
-              const double g1 = f64_red(f1[k], ar.q, ar.qinv) + f64_mulmod(x, ea, ea * ar.qinv, ar.q);
+              const double g0 = f64_red(f0[k], ar.q, ar.qinv) + f64_mulmod_h(x, eb, ar.q, ar.qinv);
+              const double g1 = f64_red(f1[k], ar.q, ar.qinv) + f64_mulmod_h(x, ea, ar.q, ar.qinv);
               f0[k] = f64_red(g0, ar.q, ar.qinv) + f64_mulmod(d0, Pd, Pq, ar.q);
               f1[k] = f64_red(g1, ar.q, ar.qinv) + f64_mulmod(d1, Pd, Pq, ar.q);
             }
@@ -239,8 +245,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
               const uint64_t d0 = mul_mod(A0, B0, mc);
               const uint64_t d1 = add_mod(mul_mod(A0, B1, mc), mul_mod(A1, B0, mc), q);
               const uint64_t c0 = a0[k] >= q ? a0[k] - q : a0[k], c1 = a1[k] >= q ? a1[k] - q : a1[k];
-              a0[k] = add_mod(c0, mul_shoup(d0, mc.pmod, mc.pmodp, q), q);
-              a1[k] = add_mod(c1, mul_shoup(d1, mc.pmod, mc.pmodp, q), q);
+              a0[k] = add_mod(c0, mul_shoup(d0, kps[2 * t], kps[2 * t + 1], q), q);
+              a1[k] = add_mod(c1, mul_shoup(d1, kps[2 * t], kps[2 * t + 1], q), q);
             }
           }
         }
@@ -253,7 +259,6 @@ __global__ void __launch_bounds__(256 * QN, 1)
       }
       // (f0, f1) / (a0, a1): this thread's words 8 th + k of slot t (natural order)
       if constexpr (KEEP) {
-        const uint64_t di = dinv[t], dip = dinvp[t];
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           const unsigned poly = 2 * p + half;
@@ -264,18 +269,16 @@ __global__ void __launch_bounds__(256 * QN, 1)
             r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
+          // out = f D^-1 - NTTrows(conv D^-1): both factors already folded in
           uint64_t o[8];
           if constexpr (F) {
-            const double dd = f64_from_u52(di), dq = dd * ar.qinv;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-              const double x = f64_red(half ? f1[k] : f0[k], ar.q, ar.qinv);  // |x - c| < 2.5 q
-              o[k] = ar.canon(f64_mulmod(x - r[k], dd, dq, ar.q));
-            }
+            for (int k = 0; k < 8; k++)
+              o[k] = ar.canon(f64_red(half ? f1[k] : f0[k], ar.q, ar.qinv) - r[k]);  // |.| < 3.1 q
           } else {
 #pragma unroll
             for (int k = 0; k < 8; k++)
-              o[k] = mul_shoup(sub_mod(half ? a1[k] : a0[k], ar.canon(r[k]), q), di, dip, q);
+              o[k] = sub_mod(half ? a1[k] : a0[k], ar.canon(r[k]), q);
           }
           ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + 8 * th);
 #pragma unroll
@@ -307,7 +310,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 
 template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW>
 static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
-                       size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl,
+                       size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl,
                        unsigned nm, unsigned t_lo, unsigned t_n)
 {
   const unsigned n = G.n, groups = t_n * (n / 2048);
@@ -322,7 +325,7 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
   const size_t t1_stride = (size_t)NDIG * nm * n;
   auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, LTW>;
   hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, T1, t1_stride, d01, evkm,
-                     dst, dst_pstride, conv, dinv, dinvp, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
+                     dst, dst_pstride, conv, ksc, kps, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
                      members, t_lo, t_n, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
@@ -330,7 +333,7 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
 template <int LOGN2>
 static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
                          const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv,
-                         const uint64_t *dinv, const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo,
+                         const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo,
                          unsigned t_n)
 {
   // LDS: the key tile (2 ndig x 16 KB) + 16 KB per quarter stream (+ 32 KB of
@@ -339,14 +342,14 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
   case 1:
     // two streams (256 VGPRs); four (1024 threads, 128 VGPRs) spilled 58-193:
     // 68.2k -> 77.6k ct-mult/s at N=2^16, L=4, dnum=1 (same box)
-    ksq_launch<LOGN2, 1, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    ksq_launch<LOGN2, 1, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
     if (allf)
-      ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+      ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
     else  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk, 60-bit set)
-      ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                                            t_lo, t_n);
     break;
   case 3:
@@ -354,10 +357,10 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
     if (allf)
-      ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                                            t_lo, t_n);
     else
-      ksq_launch<LOGN2, 3, 2, false, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm,
+      ksq_launch<LOGN2, 3, 2, false, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                                             t_lo, t_n);
     break;
   default: gpqhe_die("split key switch: %u digits", ndig);
@@ -365,20 +368,20 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
 }
 
 void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
-             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv,
-             const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
+             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
+             const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
 {
 #ifdef KSQ_DEV  // analysis builds: the bench's instantiations only
   if (logn2 == 8 && ndig == 2 && allf) {
-    ksq_launch<8, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n);
+    ksq_launch<8, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
     return;
   }
   gpqhe_die("KSQ_DEV build");
 #else
   switch (logn2) {
-  case 7: ksq_dispatch<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
-  case 8: ksq_dispatch<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
-  case 9: ksq_dispatch<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, dinv, dinvp, count, lvl, nm, t_lo, t_n); break;
+  case 7: ksq_dispatch<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
+  case 8: ksq_dispatch<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
+  case 9: ksq_dispatch<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
   default: gpqhe_die("split key switch: row length 2^%u", logn2);
   }
 #endif

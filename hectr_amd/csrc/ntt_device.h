@@ -103,6 +103,18 @@ __device__ __forceinline__ double f64_mulmod(double y, double w, double wq, doub
   return __fma_rn(-qt, q, h) + l;
 }
 
+// The same product with the quotient estimated from h itself, for a w whose
+// w / q is not at hand (twiddles staged as 8-byte entries, key words, data x
+// data products): qt = rint(fl(h) fl(1/q)) is off by < 1/2 + 1.5 |y| 2^-52,
+// the bound of a recomputed fl(w fl(1/q)) quotient, one multiply fewer.
+__device__ __forceinline__ double f64_mulmod_h(double y, double w, double q, double qinv)
+{
+  const double h = y * w;
+  const double l = __fma_rn(y, w, -h);
+  const double qt = rint(h * qinv);
+  return __fma_rn(-qt, q, h) + l;
+}
+
 __device__ __forceinline__ double f64_red(double x, double q, double qinv)
 {
   return __fma_rn(-rint(x * qinv), q, x);
@@ -222,6 +234,7 @@ struct ArInt {
   // canonical x w for a constant w < q (Shoup pair)
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t wp) const { return mul_shoup(x, w, wp, q); }
   __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t wp) const { return mulc(x, w, wp); }  // (FP64 only)
+  __device__ uint64_t canon_d(V x) const { return canon(x); }                              // (FP64 only)
 };
 
 struct ArF64 {
@@ -253,6 +266,13 @@ struct ArF64 {
   {
     const double wd = f64_from_u52(w);
     return canon(f64_mulmod(x, wd, wd / q, q));
+  }
+  // x (|x| < 2^53) as the bits of a canonical double in [0, q) (FP64 basis
+  // conversion input)
+  __device__ uint64_t canon_d(V x) const
+  {
+    const double v = f64_red(x, q, qinv);
+    return (uint64_t)__double_as_longlong(v < 0 ? v + q : v);
   }
   // x w as the bits of a canonical double in [0, q) (FP64 basis conversion input)
   __device__ uint64_t mulc_d(V x, uint64_t w, uint64_t) const
@@ -356,9 +376,15 @@ struct ArF64Row : ArF64 {
       for (int k = 0; k < E; k++) {
         if (k & half)
           continue;
-        const double2 w = twf(rt.lds, rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift));
+        const uint64_t e = rt.idx(Bs + (uint64_t)(k >> (LE - s)), shift);
         const double X = x[k];
-        double T = f64_mulmod(x[k + half], w.x, w.y, q);
+        double T;
+        if constexpr (W8) {
+          T = f64_mulmod_h(x[k + half], __longlong_as_double((long long)rt.lds[e]), q, qinv);
+        } else {
+          const double2 w = twf(rt.lds, e);
+          T = f64_mulmod(x[k + half], w.x, w.y, q);
+        }
         if (W8 && !lz && (s & 1))
           T = f64_red(T, q, qinv);  // recomputed w/q on a wide modulus: see below
         x[k] = X + T;
@@ -382,10 +408,15 @@ struct ArF64Row : ArF64 {
         for (int k = 0; k < E; k++) {
           if (k & half)
             continue;
-          const double2 w = twf(itl, rt.idx(Bs + (uint64_t)(k >> (s + 1)), shift));
+          const uint64_t e = rt.idx(Bs + (uint64_t)(k >> (s + 1)), shift);
           const double U = x[k], V_ = x[k + half];
           x[k] = U + V_;
-          x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
+          if constexpr (W8) {
+            x[k + half] = f64_mulmod_h(U - V_, __longlong_as_double((long long)itl[e]), q, qinv);
+          } else {
+            const double2 w = twf(itl, e);
+            x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
+          }
           if (W8 && !lz)  // recomputed w/q on a wide modulus: see above
             x[k + half] = f64_red(x[k + half], q, qinv);
         }
@@ -904,6 +935,7 @@ static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
 
 // Split key switch, kept / dropped basis slots (ks_split.hip): one launch of
 // ksq_kernel for row length 2^logn2 and ndig digits.
+// ksc / kps: the folded ModDown factors per basis slot (DownTable).
 void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
-             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *dinv,
-             const uint64_t *dinvp, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n);
+             const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
+             const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n);
