@@ -370,11 +370,11 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 // LDS (RowTw; FP64 moduli forward and inverse from it, integer moduli the
 // forward ones), instead of every tile re-fetching its 20 twiddle pairs per
 // thread from L2.
-// (launch bound: two workgroups per CU; the inverse then spills 16 VGPRs
-// but the roundtrip runs 7.55 -> 7.45 ms, same box; the inverse alone at one
-// workgroup per CU, no spills, ran 7.39 -> 7.50 ms)
-template <int LOGN2, bool INV, int QN, bool W8 = false, int MINW = 2 * QN>
-__global__ void __launch_bounds__(256 * QN, MINW) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
+// (launch bound: two workgroups per CU, 128 VGPRs; the inverse takes 8-byte
+// twiddle entries (W8) to fit: with 16-byte ones it spilled 16 VGPRs, and at
+// one workgroup per CU it ran slower still)
+template <int LOGN2, bool INV, int QN, bool W8 = false>
+__global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                              const ModConst *mcs, unsigned members)
 {
   using T = Row8<LOGN2>;
@@ -446,23 +446,13 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
     constexpr int QN = 2;
     const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
-    static const int var = getenv("GPQHE_NTT_INV_VARIANT") ? atoi(getenv("GPQHE_NTT_INV_VARIANT")) : 2;  // A/B (temporary)
-    if (polys >= 4 * QN && in.per == out.per && inv && var == 1) {
-      const unsigned members = std::max(1u, polys / (4 * 3));
-      hipLaunchKernelGGL((ntt_rows_q_kernel<LOGN2, true, 3, false, 3>), dim3(xcd_blocks(members, groups)), dim3(768), 0,
-                         G.stream, in, out, logn, tw, G.dev.mc, members);
-    } else if (polys >= 4 * QN && in.per == out.per && inv && var == 2) {
-      const unsigned members = std::max(1u, polys / (4 * QN));
-      hipLaunchKernelGGL((ntt_rows_q_kernel<LOGN2, true, QN, true>), dim3(xcd_blocks(members, groups)), dim3(256 * QN),
-                         0, G.stream, in, out, logn, tw, G.dev.mc, members);
-    } else if (polys >= 4 * QN && in.per == out.per && var == 3) {
-      const unsigned members = std::max(1u, polys / (4 * QN));
-      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true> : ntt_rows_q_kernel<LOGN2, false, QN, true>;
-      hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
-                         G.dev.mc, members);
-    } else if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
+    if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
       const unsigned members = std::max(1u, polys / (4 * QN));  // ~4 polys per quarter
-      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN> : ntt_rows_q_kernel<LOGN2, false, QN>;
+      // inverse: 8-byte staged twiddles (w only, quotient from the product):
+      // 94 VGPRs, no spills (16-byte entries spilled 16 at this launch bound),
+      // 107 -> 98 us per 48-poly group; the forward pass measured 86 -> 88 us
+      // with them and keeps 16-byte (w, w/q) entries
+      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
       hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
                          G.dev.mc, members);
     } else if (inv) {
