@@ -32,12 +32,20 @@ steps = []
 for a, b in zip(ends[:-1], ends[1:]):
     seg = ev[a + 1:b + 1]
     span = seg[-1][1] - ev[a][1]
-    busy = sum(e[1] - e[0] for e in seg)
+    # busy = union of the intervals (kernels of the side stream overlap)
+    busy, cur0, cur1 = 0, None, None
+    for e0, e1, *_ in sorted(seg):
+        if cur1 is None or e0 > cur1:
+            busy += (cur1 - cur0) if cur1 is not None else 0
+            cur0, cur1 = e0, e1
+        else:
+            cur1 = max(cur1, e1)
+    busy += (cur1 - cur0) if cur1 is not None else 0
     steps.append((span, busy, sum(e[2] == "K" for e in seg), sum(e[2] == "C" for e in seg), seg))
 steps = steps[len(steps) // 2:]  # steady state: the second half
 span = np.median([s[0] for s in steps]) / 1e3
 busy = np.median([s[1] for s in steps]) / 1e3
-print(f"{len(steps)} steps: span {span:.1f} us/step (D2H end to D2H end), device busy {busy:.1f} us, "
+print(f"{len(steps)} steps: span {span:.1f} us/step (D2H end to D2H end), device busy {busy:.1f} us (union), "
       f"kernels {np.median([s[2] for s in steps]):.0f}, copies {np.median([s[3] for s in steps]):.0f}")
 seg = steps[len(steps) // 2][4]
 t0 = seg[0][0]
