@@ -3,7 +3,8 @@
 
 Metric (BASELINE.json): ct x ct + relinearization (+ rescale) per second at
 N = 2^16, L = 8 RNS primes (configs[2]: batch = 256 ciphertext pairs per GPU,
-one step = one batch through he_mul_rescale_batch).  Inputs are synthetic
+one step = one batch through he_mul_rescale_batch, run as two 128-pair
+sub-chunks on two HIP streams, gpqhe_set_streams).  Inputs are synthetic
 random-residue ciphertexts already resident in HBM (poly_fill_uniform,
 splitmix64 streams); the relinearization key is a real key (he_genrlk).
 
@@ -69,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--c5-batch", type=int, default=64)
     ap.add_argument("--ntt-polys", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample duration per thread count")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-chunks of a batch on their own HIP streams (gpqhe_set_streams: 1 or 2)")
     ap.add_argument("--launch-check", action="store_true",
                     help="run only the multi-process launch / rendezvous / reduction path (no engine, no GPU)")
     return ap.parse_args(argv)
@@ -500,13 +503,17 @@ def main():
     stream = torch.cuda.Stream()
     mb = MulBatch(stream, logn, L, dnum, args.q0_bits, args.p_bits, args.nspecial, B, rank * B, 1000 + rank)
     eng = mb.eng
+    eng.lib.gpqhe_set_streams(args.streams)
     elapsed = timed(mb.step, args.steps, args.warmup, eng.sync, barrier)
     elapsed = hdist.max_over_ranks(elapsed, device=red_dev)
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
     # instrumented pass (same steps): per-kernel device time from HIP events on
-    # the engine stream, streamed bytes per launch from the library
+    # the engine stream, streamed bytes per launch from the library -- with
+    # the batch as one chunk on one stream, so each kernel's launch time is
+    # its own (two streams overlap the kernels of the two sub-chunks)
+    eng.lib.gpqhe_set_streams(1)
     eng.prof_enable(True)
     ti0 = time.perf_counter()
     for _ in range(args.steps):
@@ -515,6 +522,7 @@ def main():
     ti1 = time.perf_counter()
     stats = eng.prof_collect()
     eng.prof_enable(False)
+    eng.lib.gpqhe_set_streams(args.streams)
     step_s = (ti1 - ti0) / args.steps
     launches_per_step = stats[max(stats, key=lambda k: stats[k][1])][0] / args.steps
     pairs_per_launch = int(round(B / launches_per_step))
@@ -547,6 +555,7 @@ def main():
                        "batch_per_gpu": B, "logn": logn, "nlimbs": L, "nspecial": mb.K,
                        "dnum": mb.dnum, "prime_bits": {"q0": args.q0_bits, "qi": 50, "p": args.p_bits},
                        "pairs_per_launch": pairs_per_launch,
+                       "streams": args.streams,
                        "parallelism": f"batch-sharded x{world}"},
             "per_gpu_value": value / world,
             "op_roofline": {"alg_bytes_per_op": alg, "achieved_GBs": alg * value / world / 1e9,
@@ -564,6 +573,7 @@ def main():
         # the conventional prime sizes (60-bit q0 and special primes: the
         # integer butterflies on those limbs), same op, batch and harness
         alt = MulBatch(stream, logn, L, dnum, args.alt_bits, args.alt_bits, 0, B, rank * B, 1000 + rank)
+        alt.eng.lib.gpqhe_set_streams(args.streams)
         t = hdist.max_over_ranks(timed(alt.step, args.steps, 1, alt.eng.sync, barrier), device=red_dev)
         if rank == 0:
             v = world * B * args.steps / t
@@ -578,6 +588,7 @@ def main():
         # config 5: n = 2^17, L = 12 (dnum 3, K 4, conventional primes), each
         # rank its own shard of the global batch
         c5 = MulBatch(stream, 17, 12, 3, 60, 60, 4, args.c5_batch, rank * args.c5_batch, 2000 + rank)
+        c5.eng.lib.gpqhe_set_streams(args.streams)
         steps5 = max(2, args.steps // 2)
         t = hdist.max_over_ranks(timed(c5.step, steps5, 1, c5.eng.sync, barrier), device=red_dev)
         if rank == 0:

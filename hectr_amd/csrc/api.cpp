@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <string>
 #include <unordered_map>
 
@@ -1535,6 +1536,15 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
 // ===========================================================================
 // Batched entry points
 // ===========================================================================
+static unsigned g_mul_streams = 2;  // he_mul_rescale_batch: sub-chunks on their own streams (1 or 2)
+
+extern "C" void gpqhe_set_streams(unsigned int n)
+{
+  if (n != 1 && n != 2)
+    gpqhe_die("gpqhe_set_streams: 1 or 2, not %u", n);
+  g_mul_streams = n;
+}
+
 extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uint64_t *b, size_t count,
                                      unsigned int nlimbs, const he_evk_t *rlk)
 {
@@ -1563,6 +1573,45 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   if (nchunks)
     chunk = (count + nchunks - 1) / nchunks;
   const size_t in_stride = 2 * lvl * n, out_stride = 2 * (size_t)(lvl - 1) * n;
+  // Two sub-chunks on two streams, the second started once the first's
+  // d2_rows has run, so one's VALU-bound column kernels overlap the other's
+  // HBM-bound kernels on the same CUs (same box: 42.1k -> 42.7k ct-mult/s,
+  // 60-bit 32.3k -> 32.7k, config 5 7.87k -> 7.98k; three or four streams
+  // and four or more sub-chunks were slower).  Only without aliasing: a
+  // sub-chunk's output must not overlap the other's inputs.
+  const unsigned nsub = g_mul_streams;
+  const uint64_t *oend = out + count * out_stride, *aend = a + count * in_stride, *bend = b + count * in_stride;
+  const bool alias = (out < aend && a < oend) || (out < bend && b < oend);
+  if (nsub == 2 && count >= 2 && nchunks == 1 && !alias && k_mul_split_ok(lvl) && rlk->reserved &&
+      rlk->dnum == G.dnum) {
+    static hipStream_t s2 = nullptr;
+    static hipEvent_t ev_fork, ev_d2, ev_join;
+    if (!s2) {
+      HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&ev_d2, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
+    const unsigned c1 = (unsigned)(count / 2), c2 = (unsigned)(count - c1);
+    // both workspaces come from the engine stream's pool before the fork and
+    // go back to it after the join
+    Ws w1(k_mul_split_ws_words(c1, lvl, true)), w2(k_mul_split_ws_words(c2, lvl, true));
+    HIP_CHECK(hipEventRecord(ev_fork, G.stream));
+    HIP_CHECK(hipStreamWaitEvent(s2, ev_fork, 0));
+    g_split_after_d2 = ev_d2;
+    k_mul_relin_split(out, (lvl - 1) * n, a, b, in_stride, lvl * n, evkm, c1, lvl, true, w1.p);
+    g_split_after_d2 = nullptr;
+    HIP_CHECK(hipStreamWaitEvent(s2, ev_d2, 0));
+    const hipStream_t eng = G.stream;
+    G.stream = s2;
+    k_mul_relin_split(out + c1 * out_stride, (lvl - 1) * n, a + c1 * in_stride, b + c1 * in_stride, in_stride,
+                      lvl * n, evkm, c2, lvl, true, w2.p);
+    G.stream = eng;
+    HIP_CHECK(hipEventRecord(ev_join, s2));
+    HIP_CHECK(hipStreamWaitEvent(G.stream, ev_join, 0));
+    return;
+  }
   for (size_t c0 = 0; c0 < count; c0 += chunk) {
     const unsigned cnt = (unsigned)std::min(chunk, count - c0);
     mul_chunk(out + c0 * out_stride, (lvl - 1) * n, a + c0 * in_stride, b + c0 * in_stride, in_stride, lvl * n, cnt,

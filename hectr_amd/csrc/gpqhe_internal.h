@@ -373,6 +373,7 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d2, uint64_t *ybuf, uint64
 // conversion, then the kept slots' inner product with the ModDown epilogue).
 // out may equal a or b only with one pair and out_pstride == in_pstride.
 bool k_mul_split_ok(unsigned lvl);
+extern hipEvent_t g_split_after_d2;  // recorded after d2_rows when set (experiment)
 // ws: a workspace of k_mul_split_ws_words(count, lvl, rescale) words, or null
 // (the pool's, on the engine stream)
 size_t k_mul_split_ws_words(unsigned count, unsigned lvl, bool rescale);

@@ -3468,6 +3468,8 @@ bool k_mul_split_ok(unsigned lvl)
   return k_ks_fused_ok() && split_ndig_ok(ndig);
 }
 
+hipEvent_t g_split_after_d2 = nullptr;
+
 template <int LOGT1, int LOGN2>
 static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
                              size_t in_stride, size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl,
@@ -3491,6 +3493,8 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   const D01Src d01{a, b, in_stride, in_pstride};
   const bool allf = up.f64 && dn.f64;
   d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc);
+  if (g_split_after_d2)  // (experiment: two-stream pipelining)
+    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
   ks_cols_stage<LOGT1>(y, T1, count, lvl, invc);
   {
     // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per

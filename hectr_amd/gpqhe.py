@@ -97,6 +97,7 @@ SIGNATURES = {
     "hectx_info": (None, [P(Info)]),
     "gpqhe_set_seed": (None, [C.c_uint64]),
     "gpqhe_set_stream": (None, [VP]),
+    "gpqhe_set_streams": (None, [C.c_uint]),
     "gpqhe_sync": (None, []),
     "he_alloc_pk": (None, [OBJ]), "he_free_pk": (None, [OBJ]),
     "he_alloc_sk": (None, [OBJ]), "he_free_sk": (None, [OBJ]),

@@ -127,6 +127,11 @@ void gpqhe_set_seed(uint64_t seed);                   /* [ext] reset RNG  */
  * Ignored by the oracle. */
 void gpqhe_set_stream(void *stream);
 void gpqhe_sync(void);                                /* [ext] */
+/* [ext] he_mul_rescale_batch: run a batch as 1 or 2 sub-chunks on their own
+ * HIP streams (default 2: one sub-chunk's compute-bound kernels overlap the
+ * other's memory-bound ones).  Bits never depend on it; ignored by the
+ * oracle. */
+void gpqhe_set_streams(unsigned int n);
 
 /* ------------------------------------------------------------------------ */
 /* Allocation: reference src/ctr.c:461-465,524-527,537-541,608-616;         */

@@ -451,6 +451,11 @@ void gpqhe_set_stream(void *stream)
   (void)stream;
 }
 
+void gpqhe_set_streams(unsigned int n)
+{
+  (void)n;
+}
+
 void gpqhe_sync(void)
 {
 }

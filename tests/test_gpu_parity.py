@@ -266,6 +266,19 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
 
 
+@pytest.mark.parametrize("streams", [1, 2])
+def test_mul_rescale_batch_streams(oracle, product, streams):
+    """The batch as one chunk on the engine stream (gpqhe_set_streams(1)) and
+    as two sub-chunks on two streams, the second started after the first's
+    d2_rows (the default): identical residues either way, odd split 12 + 13."""
+    product.lib.gpqhe_set_streams(streams)
+    try:
+        want, got = mul_batch_both(oracle, product, "bench51", 25, seeds=(31, 32))
+    finally:
+        product.lib.gpqhe_set_streams(2)
+    assert np.array_equal(got, want), f"{np.count_nonzero(got != want)} residues differ"
+
+
 @pytest.mark.parametrize("name", ["bench_d2", "bench51"])
 def test_batch_real_encryptions_decode(product, name):
     """a 4-ciphertext subset of real encryptions of
