@@ -169,15 +169,17 @@ static void stage_release()
 struct PendEcd {
   uint64_t *dst;
   unsigned lvl, slots;
+  size_t coff;  // its 2 slots coefficient values at g_pcoef + coff (hm_encode_slots)
 };
 struct PendEnc {
   uint64_t *c0, *c1;
   const uint64_t *m, *pk0, *pk1;
   unsigned lvl;
   uint64_t stream;
+  int ecd;  // m is queued encode ecd (its coefficients join e0: EncCoef), else -1
 };
 static std::vector<PendEcd> g_pecd;
-static std::vector<int64_t> g_pcoef;  // n coefficients per pending encode
+static std::vector<int64_t> g_pcoef;  // 2 slots coefficient values per pending encode
 static std::vector<PendEnc> g_penc;
 
 // he_gemv is queued the same way (at most two, run as one batch: the two
@@ -286,11 +288,33 @@ static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
   o->data = (uint64_t *)pool_alloc(bytes);
 }
 
+// Freeing the target of a queued encode that no other queued work reads
+// (HECTR frees its five plaintexts right after encrypting them, src/ctr.c:
+// 476-480; the queued encryptions take the coefficients, not the payload):
+// the encode is dropped instead of flushing the queue.  True if so.
+static bool drop_dead_encode(const uint64_t *data)
+{
+  if (!data || !g_pgemv.empty() || g_pew.count)
+    return false;
+  bool target = false;
+  for (const PendEcd &e : g_pecd)
+    target |= e.dst == data;
+  if (!target)
+    return false;
+  for (const PendEnc &e : g_penc)
+    if (e.c0 == data || e.c1 == data || e.pk0 == data || e.pk1 == data || (e.m == data && e.ecd < 0))
+      return false;
+  for (PendEcd &e : g_pecd)
+    if (e.dst == data)
+      e.dst = nullptr;
+  return true;
+}
+
 static void obj_free(void *vo)
 {
   // a queued encode / encryption / gemv may still use the payload (queued
   // elementwise ops keep their order with any later user of the block)
-  if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty()))
+  if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty()) && !drop_dead_encode(OB(vo)->data))
     check_ctx();
   he_ct_t *o = OB(vo);
   if (o->data && G.init)
@@ -729,52 +753,68 @@ static void flush_pending()
 {
   std::vector<PendEcd> ecd;
   std::vector<PendEnc> enc;
-  std::vector<int64_t> coef;
+  std::vector<int64_t> vals;
   ecd.swap(g_pecd);
   enc.swap(g_penc);
-  coef.swap(g_pcoef);
+  vals.swap(g_pcoef);
   const size_t n = G.n;
-  if (!ecd.empty()) {
-    // an encoding of s slots is zero off the stride n / 2s: upload only the
-    // coefficients on the widest stride every queued encode shares
-    unsigned clog = G.logn;
-    for (const PendEcd &e : ecd)
-      clog = std::min(clog, (unsigned)__builtin_ctz(G.n / (2 * e.slots)));
-    const size_t row = n >> clog;
-    for (size_t i = 0; i < ecd.size(); i++)
-      for (size_t j = 0; j < row; j++)
-        coef[i * row + j] = coef[i * n + (j << clog)];
-    // up to CoefArg::MAX values (HECTR's step: 5 x 32) they travel in the
-    // kernel arguments; up to 64 KB the lift kernels read them straight from
-    // pinned host memory; more is uploaded first
-    const size_t cbytes = ecd.size() * row * 8;
-    const bool arg = ecd.size() * row <= CoefArg::MAX, zc = !arg && cbytes <= 65536;
-    Ws up(arg || zc ? 0 : ecd.size() * row);
-    const void *dmap = up.p;
-    Stage *st = zc ? &stage_map(coef.data(), cbytes, &dmap) : nullptr;
-    if (!arg && !zc)
-      upload(up.p, coef.data(), cbytes);
-    const int64_t *dcoef = (const int64_t *)dmap;
-    for (size_t i0 = 0; i0 < ecd.size();) {
-      // one launch per run of equal levels (at most GPQHE_MAXGRP polys)
-      size_t i1 = i0 + 1;
-      while (i1 < ecd.size() && i1 - i0 < GPQHE_MAXGRP && ecd[i1].lvl == ecd[i0].lvl)
-        i1++;
-      unsigned mods[GPQHE_MAXMOD];
-      for (unsigned l = 0; l < ecd[i0].lvl; l++)
-        mods[l] = l;
-      LimbSet ls = limbset(nullptr, mods, ecd[i0].lvl, (unsigned)(i1 - i0), 0);
-      ls.ngp = (uint32_t)(i1 - i0);
-      for (size_t i = i0; i < i1; i++)
-        ls.gp[i - i0] = ecd[i].dst;
-      if (arg)
-        k_lift_ntt_arg(ls, coef.data() + i0 * row, clog);
-      else
-        k_lift_ntt(ls, dcoef + i0 * row, clog);
-      i0 = i1;
+  // an encoding of s slots is zero off the stride n / 2s: the launches take
+  // one row of the coefficients on the widest stride every queued encode
+  // shares (value j = coefficient j 2^clog)
+  unsigned clog = G.logn;
+  for (const PendEcd &e : ecd)
+    clog = std::min(clog, (unsigned)__builtin_ctz(G.n / (2 * e.slots)));
+  const size_t row = n >> clog;
+  std::vector<int64_t> coef(ecd.size() * row);
+  for (size_t i = 0; i < ecd.size(); i++) {
+    const size_t step = (n / (2 * ecd[i].slots)) >> clog;
+    for (size_t t = 0; t < 2 * (size_t)ecd[i].slots; t++)
+      coef[i * row + t * step] = vals[ecd[i].coff + t];
+  }
+  // a device-readable copy of the rows, made when a launch needs more values
+  // than travel in its arguments: up to 64 KB the kernels read pinned host
+  // memory, more is uploaded
+  const size_t cbytes = ecd.size() * row * 8;
+  Ws up(0);
+  Stage *st = nullptr;
+  const int64_t *dcoef = nullptr;
+  auto dev_coef = [&]() {
+    if (!dcoef) {
+      if (cbytes <= 65536) {
+        const void *dmap = nullptr;
+        st = &stage_map(coef.data(), cbytes, &dmap);
+        dcoef = (const int64_t *)dmap;
+      } else {
+        up.p = (uint64_t *)pool_alloc(cbytes);
+        upload(up.p, coef.data(), cbytes);
+        dcoef = (const int64_t *)up.p;
+      }
     }
-    if (st)
-      stage_done(*st);
+    return dcoef;
+  };
+  // the encodes whose plaintext still lives (dropped ones: drop_dead_encode)
+  for (size_t i0 = 0; i0 < ecd.size();) {
+    if (!ecd[i0].dst) {
+      i0++;
+      continue;
+    }
+    // one launch per run of live encodes at equal levels (at most GPQHE_MAXGRP)
+    size_t i1 = i0 + 1;
+    while (i1 < ecd.size() && i1 - i0 < GPQHE_MAXGRP && ecd[i1].dst && ecd[i1].lvl == ecd[i0].lvl)
+      i1++;
+    unsigned mods[GPQHE_MAXMOD];
+    for (unsigned l = 0; l < ecd[i0].lvl; l++)
+      mods[l] = l;
+    LimbSet ls = limbset(nullptr, mods, ecd[i0].lvl, (unsigned)(i1 - i0), 0);
+    ls.ngp = (uint32_t)(i1 - i0);
+    for (size_t i = i0; i < i1; i++)
+      ls.gp[i - i0] = ecd[i].dst;
+    // up to CoefArg::MAX values (HECTR's step: 5 x 32) in the kernel arguments
+    if ((i1 - i0) * row <= CoefArg::MAX)
+      k_lift_ntt_arg(ls, coef.data() + i0 * row, clog);
+    else
+      k_lift_ntt(ls, dev_coef() + i0 * row, clog);
+    i0 = i1;
   }
   for (size_t i0 = 0; i0 < enc.size();) {
     // a run of encryptions at one level with consecutive RNG streams and the
@@ -788,19 +828,41 @@ static void flush_pending()
     unsigned mods[GPQHE_MAXMOD];
     for (unsigned l = 0; l < lvl; l++)
       mods[l] = l;
+    // plaintexts that are queued encodes join e0 as coefficients (EncCoef):
+    // the combine then reads no NTT-form plaintext
+    EncCoef ec{};
+    ec.clog = clog;
+    ec.row = (uint32_t)row;
+    unsigned nrows = 0;
+    for (unsigned e = 0; e < k; e++)
+      ec.row_of[e] = enc[i0 + e].ecd;
+    for (unsigned e = 0; e < k; e++)
+      nrows += enc[i0 + e].ecd >= 0;
+    if (nrows * row <= EncCoef::MAX) {
+      unsigned r = 0;
+      for (unsigned e = 0; e < k; e++)
+        if (enc[i0 + e].ecd >= 0) {
+          memcpy(ec.v + r * row, coef.data() + (size_t)enc[i0 + e].ecd * row, row * 8);
+          ec.row_of[e] = (int32_t)r++;
+        }
+    } else {
+      ec.p = dev_coef();
+    }
     Ws vee(3 * k * w);
     LimbSet s = limbset(vee.p, mods, lvl, 3 * k, w);
-    k_sample_enc(s, enc[i0].stream, 3 * k);
+    k_sample_enc(s, enc[i0].stream, 3 * k, nrows ? &ec : nullptr);
     k_ntt(s, false);
     EncBatch b{};
     for (unsigned e = 0; e < k; e++) {
       b.c0[e] = enc[i0 + e].c0;
       b.c1[e] = enc[i0 + e].c1;
-      b.m[e] = enc[i0 + e].m;
+      b.m[e] = enc[i0 + e].ecd >= 0 ? nullptr : enc[i0 + e].m;
     }
     k_enc_combine_batch(b, k, vee.p, enc[i0].pk0, enc[i0].pk1, lvl);
     i0 = i1;
   }
+  if (st)
+    stage_done(*st);
 }
 
 static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scale, const unsigned *mods,
@@ -842,10 +904,12 @@ extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int s
       busy |= e.dst == pt->data;
     if (busy)
       flush_pending();
+    if (slots > G.n / 2)
+      gpqhe_die("bad slot count %u", slots);
     const size_t at = g_pcoef.size();
-    g_pcoef.resize(at + G.n);
-    hm_encode_coeffs(g_pcoef.data() + at, (const double *)z, slots, G.n, scale);
-    g_pecd.push_back({pt->data, nlimbs, slots});
+    g_pcoef.resize(at + 2 * (size_t)slots);
+    hm_encode_slots(g_pcoef.data() + at, (const double *)z, slots, scale);
+    g_pecd.push_back({pt->data, nlimbs, slots, at});
   } else {
     unsigned mods[GPQHE_MAXMOD];
     for (unsigned i = 0; i < nlimbs; i++)
@@ -949,7 +1013,13 @@ extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
     const uint64_t stream = next_stream();
     next_stream();
     next_stream();
-    g_penc.push_back({limb(ct, 0, 0), limb(ct, 1, 0), pt->data, limb(pk, 0, 0), limb(pk, 1, 0), lvl, stream});
+    // a plaintext that is itself a queued encode (at this level) joins e0 as
+    // coefficients (EncCoef)
+    int ei = -1;
+    for (size_t i = 0; i < g_pecd.size(); i++)
+      if (g_pecd[i].dst == pt->data && g_pecd[i].lvl == lvl)
+        ei = (int)i;
+    g_penc.push_back({limb(ct, 0, 0), limb(ct, 1, 0), pt->data, limb(pk, 0, 0), limb(pk, 1, 0), lvl, stream, ei});
     ct->nlimbs = lvl;
     ct->scale = pt->scale;
     ct->flags = 0;
@@ -1283,6 +1353,17 @@ static std::unordered_map<std::string, uint64_t *> g_gemv_cache;
 static std::vector<void *> g_gemv_blocks;  // what the cache's entries live in (one entry or a batch)
 static size_t g_gemv_cache_bytes = 0;
 
+// Whole matrices already seen (HECTR passes the same two gain matrices every
+// step): the non-zero diagonals' rotations and cached encodings, so a repeat
+// he_gemv costs one compare of the matrix instead of s diagonal keys.
+struct GemvMat {
+  unsigned s, lvl;
+  std::vector<double> M;
+  std::vector<GemvDiags> dgs;  // evk filled per call from its rk
+  std::vector<unsigned> rot;   // the rotation of each diagonal, in dgs order
+};
+static std::vector<GemvMat> g_gemv_mats;
+
 void gemv_cache_clear()
 {
   for (void *b : g_gemv_blocks)
@@ -1290,6 +1371,7 @@ void gemv_cache_clear()
   g_gemv_blocks.clear();
   g_gemv_cache.clear();
   g_gemv_cache_bytes = 0;
+  g_gemv_mats.clear();
 }
 
 static std::string diag_key(const double *diag, unsigned s, unsigned lvl)
@@ -1451,6 +1533,23 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
       flush_gemvs();
   }
   PendGemv pg{y->data, pstride(y), limb(x, 0, 0), limb(x, 1, 0), x->data, lvl, {}};
+  const size_t mwords = 2 * (size_t)s * s;
+  for (const GemvMat &gm : g_gemv_mats)
+    if (gm.s == s && gm.lvl == lvl && !memcmp(gm.M.data(), Md, mwords * 8)) {
+      size_t r = 0;
+      pg.dgs = gm.dgs;
+      for (GemvDiags &dg : pg.dgs)
+        for (unsigned e = 0; e < dg.count; e++, r++)
+          dg.evk[e] = gm.rot[r] ? find_rot_key(rk, gm.rot[r], dg.g[e])->data : nullptr;
+      g_pgemv.push_back(std::move(pg));
+      if (!defer)
+        flush_gemvs();
+      y->nlimbs = lvl - 1;
+      y->scale = x->scale;
+      y->flags = 0;
+      return;
+    }
+  std::vector<unsigned> rots;
   std::vector<double> diag(2 * (size_t)s);
   // diagonals not cached yet (host-FFT sizes) are encoded together after the
   // loop: one upload and one lift + NTT launch for all of them
@@ -1502,6 +1601,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     dg.evk[dg.count] = k ? k->data : nullptr;
     dg.pt[dg.count] = pt;
     dg.g[dg.count] = g;
+    rots.push_back(d);
     if (++dg.count == GemvDiags::MAX) {
       pg.dgs.push_back(dg);
       dg.count = 0;
@@ -1524,6 +1624,9 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     for (const Fix &f : fixes)
       pg.dgs[f.launch].pt[f.e] = slab + (size_t)f.idx * per;
   }
+  if (g_gemv_mats.size() >= 8)
+    g_gemv_mats.erase(g_gemv_mats.begin());
+  g_gemv_mats.push_back({s, lvl, std::vector<double>(Md, Md + mwords), pg.dgs, rots});
   const double scale = x->scale;
   g_pgemv.push_back(std::move(pg));
   if (!defer)

@@ -233,6 +233,9 @@ void hm_fft_tables(unsigned s, double *ksi, unsigned *rot);
 // operations, same order: bit-identical).  Synchronises (overflow check).
 void k_encode_coeffs(int64_t *coef, double *work, unsigned s, double scale);
 void hm_encode_coeffs(int64_t *coef, const double *z_interleaved, unsigned s, unsigned n, double scale);
+// The 2s non-zero coefficients of that encoding only: v[k] is coefficient
+// k n / 2s (the same values, no n-word array).
+void hm_encode_slots(int64_t *v, const double *z_interleaved, unsigned s, double scale);
 // GPU decoder: z (device, s complex values) <- the centred CRT lift of the
 // coefficient limbs coef [nl][n] (device), / scale, forward special FFT --
 // bit-identical to the oracle's he_dcd; asynchronous on the engine stream.
@@ -282,7 +285,19 @@ void k_ew_prog(const EwProg &p);
 // s <= GPQHE_DCD_ONEPASS, n = 2^10 .. 2^12) in one more launch; c: nl n
 // words of workspace; z as k_decode's.
 void k_ew_decode(const EwProg &p, double *z, const uint64_t *pt, unsigned nl, unsigned s, double scale, uint64_t *c);
-void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly);
+// Plaintext coefficients added to the queued encryptions' e0 before their
+// transform (NTT(e0 + m) = NTT(e0) + NTT(m) mod q): the combine then needs no
+// NTT-form plaintext.  Encryption e of a launch takes row row_of[e] (-1: none),
+// n >> clog values per row (value j is coefficient j 2^clog, the others are
+// 0), from v (by value) or, when p is set, from device-readable memory.
+struct EncCoef {
+  static constexpr unsigned MAX = 320;
+  int64_t v[MAX];
+  const int64_t *p;
+  int32_t row_of[GPQHE_MAXGRP];
+  uint32_t clog, row;
+};
+void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly, const EncCoef *ec = nullptr);
 void k_sample_small(const LimbSet &dst, uint64_t stream, int cbd);
 void k_sample_uniform(const LimbSet &dst, uint64_t stream);
 void k_lift_i64(const LimbSet &dst, const int64_t *coef);
@@ -303,7 +318,7 @@ void k_enc_combine(uint64_t *c0, uint64_t *c1, const uint64_t *v, const uint64_t
 // v, e0, e1 from vee + (3 i + {0, 1, 2}) * lvl * n
 struct EncBatch {
   uint64_t *c0[GPQHE_MAXGRP], *c1[GPQHE_MAXGRP];
-  const uint64_t *m[GPQHE_MAXGRP];
+  const uint64_t *m[GPQHE_MAXGRP];  // nullptr: m was added to e0 (EncCoef)
 };
 void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, const uint64_t *pk0,
                          const uint64_t *pk1, unsigned lvl);

@@ -17,6 +17,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
+#include <memory>
+
 typedef unsigned __int128 u128;
 
 void gpqhe_die(const char *fmt, ...)
@@ -167,9 +170,20 @@ struct FftTables {
 
 // Tables of the special FFT for s slots, for the GPU encoder: ksi[k] =
 // exp(2 pi i k / 4s) for k <= 4s as (re, im) pairs, rot[j] = 5^j mod 4s.
+// The tables of one slot count, built once: the control loop encodes at one
+// size every step, and 4s + 1 cos / sin pairs cost more than its FFT.
+static const FftTables &fft_tables(unsigned s)
+{
+  static std::map<unsigned, std::unique_ptr<FftTables>> cache;
+  std::unique_ptr<FftTables> &t = cache[s];
+  if (!t)
+    t.reset(new FftTables(s));
+  return *t;
+}
+
 void hm_fft_tables(unsigned s, double *ksi, unsigned *rot)
 {
-  FftTables T(s);
+  const FftTables &T = fft_tables(s);
   for (unsigned k = 0; k <= 4 * s; k++) {
     ksi[2 * k] = T.ksi[k].re;
     ksi[2 * k + 1] = T.ksi[k].im;
@@ -193,7 +207,7 @@ static void bitrev_perm(cplx *v, unsigned s)
 
 static void fft_special_enc(cplx *v, unsigned s)
 {
-  FftTables T(s);
+  const FftTables &T = fft_tables(s);
   const unsigned M = 4 * s;
   for (unsigned len = s; len >= 2; len >>= 1) {
     const unsigned h = len >> 1, lq = len << 2;
@@ -212,21 +226,31 @@ static void fft_special_enc(cplx *v, unsigned s)
     v[i] = {v[i].re / (double)s, v[i].im / (double)s};
 }
 
-void hm_encode_coeffs(int64_t *coef, const double *z, unsigned s, unsigned n, double scale)
+void hm_encode_slots(int64_t *v, const double *z, unsigned s, double scale)
 {
-  if (!s || (s & (s - 1)) || s > n / 2)
+  if (!s || (s & (s - 1)))
     gpqhe_die("bad slot count %u", s);
   std::vector<cplx> u(s);
   for (unsigned i = 0; i < s; i++)
     u[i] = {z[2 * i], z[2 * i + 1]};
   fft_special_enc(u.data(), s);
-  memset(coef, 0, (size_t)n * sizeof(int64_t));
-  const unsigned gap = n / (2 * s);
   for (unsigned k = 0; k < s; k++) {
     const double re = u[k].re * scale, im = u[k].im * scale;
     if (fabs(re) >= 9.2e18 || fabs(im) >= 9.2e18)
       gpqhe_die("encode overflow (|value * scale| >= 2^63)");
-    coef[(size_t)k * gap] = llround(re);
-    coef[(size_t)(k + s) * gap] = llround(im);
+    v[k] = llround(re);
+    v[k + s] = llround(im);
   }
+}
+
+void hm_encode_coeffs(int64_t *coef, const double *z, unsigned s, unsigned n, double scale)
+{
+  if (!s || (s & (s - 1)) || s > n / 2)
+    gpqhe_die("bad slot count %u", s);
+  std::vector<int64_t> v(2 * (size_t)s);
+  hm_encode_slots(v.data(), z, s, scale);
+  memset(coef, 0, (size_t)n * sizeof(int64_t));
+  const unsigned gap = n / (2 * s);
+  for (unsigned k = 0; k < 2 * s; k++)
+    coef[(size_t)k * gap] = v[k];
 }

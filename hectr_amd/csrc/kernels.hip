@@ -528,104 +528,7 @@ __device__ __forceinline__ uint64_t lift_i64(int64_t v, const ModConst &c)
   return r == c.q ? 0 : c.q - r;
 }
 
-// The rounds as device functions: the first loads and the last stores are the
-// caller's (load(k, i) -> V, store(k, i, V) for element i held in slot k).
-// The last inverse round and the first forward round both give thread th the
-// elements th + k n/8 (k < 8), so a caller can finish an inverse transform,
-// combine per element in registers and start a forward transform on the
-// result without an LDS pass (modup_small_kernel, moddown_small_kernel).
-template <int LOGN, class A, class LD, class ST>
-__device__ __forceinline__ void small_fwd(const A &ar, uint64_t *lds, LD &&load, ST &&store)
-{
-  using V = typename A::V;
-  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
-  const int th = threadIdx.x;
-  V a[8];
-#pragma unroll
-  for (int r = 0; r < FULL; r++) {
-    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      a[k] = r ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
-    ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
-    if (r + 1 < FULL || REM) {
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        lds[pos0 + k * d8] = A::bits(a[k]);
-      __syncthreads();
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        store(k, pos0 + k * d8, a[k]);
-    }
-  }
-  if constexpr (REM > 0) {
-    // last REM stages (distances 2^(REM-1) .. 1): thread t owns 8
-    // consecutive elements = 8 / 2^REM groups
-    constexpr int EG = 1 << REM;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      a[k] = A::unbits(lds[8 * th + k]);
-#pragma unroll
-    for (int j = 0; j < 8 / EG; j++) {
-      V g[EG];
-#pragma unroll
-      for (int e = 0; e < EG; e++)
-        g[e] = a[j * EG + e];
-      ar.template fwd<REM>(g, (uint64_t)n + 8 * th + EG * j, REM - 1);
-#pragma unroll
-      for (int e = 0; e < EG; e++)
-        store(j * EG + e, 8 * th + j * EG + e, g[e]);
-    }
-  }
-}
-
-template <int LOGN, class A, class LD, class ST>
-__device__ __forceinline__ void small_inv(const A &ar, uint64_t *lds, LD &&load, ST &&store)
-{
-  using V = typename A::V;
-  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
-  const int th = threadIdx.x;
-  V a[8];
-  if constexpr (REM > 0) {
-    constexpr int EG = 1 << REM;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      a[k] = load(k, 8 * th + k);
-#pragma unroll
-    for (int j = 0; j < 8 / EG; j++) {
-      V g[EG];
-#pragma unroll
-      for (int e = 0; e < EG; e++)
-        g[e] = a[j * EG + e];
-      ar.template inv<REM>(g, (uint64_t)n + 8 * th + EG * j, 0);
-#pragma unroll
-      for (int e = 0; e < EG; e++)
-        lds[8 * th + j * EG + e] = A::bits(g[e]);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int rr = 0; rr < FULL; rr++) {
-    const int r = FULL - 1 - rr;  // smallest distances first
-    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      a[k] = (rr || REM) ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
-    ar.template inv<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 3);
-    if (rr + 1 < FULL) {
-      __syncthreads();  // every group of this round has read its inputs
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        lds[pos0 + k * d8] = A::bits(a[k]);
-      __syncthreads();
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        store(k, pos0 + k * d8, a[k]);
-    }
-  }
-}
+// small_fwd / small_inv: ntt_device.h
 
 template <int LOGN, bool INV>
 __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const ModConst *mcs,
@@ -679,7 +582,11 @@ __global__ void __launch_bounds__(512) lift_ntt_arg_kernel(LimbSet s, Tw2 tw, co
     small_fwd<LOGN>(
         ar, lds,
         [&](int, int i) {
-          return A::load((i & ((1 << clog) - 1)) ? 0 : lift_i64(ca.v[g * ca.row + (i >> clog)], mc));
+          // round 0 holds elements th + k n/8: for clog >= 6 the value index
+          // i >> clog is wave-uniform, so a scalar load reads the argument
+          // (per-lane reads of by-value arguments cost ~3.5 us, ubench_small)
+          const int j = clog >= 6 ? __builtin_amdgcn_readfirstlane(i >> clog) : i >> clog;
+          return A::load((i & ((1 << clog) - 1)) ? 0 : lift_i64(ca.v[g * ca.row + j], mc));
         },
         [&](int, int i, typename A::V a) { x[i] = ar.canon(a); });
   });
@@ -1051,8 +958,11 @@ __global__ void sample_small_kernel(LimbSet dst, unsigned logn, ChachaKey key, u
 // Encryption noise in one launch: polynomial y of `npoly` (rows of dst.per
 // limbs) draws from ChaCha stream `stream + y`; y = 0 is ternary (v), the
 // others CBD (e0, e1) -- the same streams and values as npoly separate
-// k_sample_small calls in that order.
-__global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, const ModConst *mc)
+// k_sample_small calls in that order.  With ec, encryption e's e0 (y = 3 e + 1)
+// also takes the integer coefficients of its plaintext (EncCoef): the caller
+// then combines without m, as NTT(e0 + m) = NTT(e0) + NTT(m) mod q.
+__global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, const ModConst *mc,
+                                  EncCoef ec, int has_ec)
 {
   const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= (1u << logn))
@@ -1067,16 +977,32 @@ __global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uin
     const uint32_t r = b[0] & 3u;
     v = r < 2 ? 0 : (r == 2 ? 1 : -1);
   }
+  bool addm = false;
+  int64_t mco = 0;
+  if (has_ec && y % 3 == 1) {
+    const int row = ec.row_of[y / 3];
+    if (row >= 0 && !(k & ((1u << ec.clog) - 1))) {
+      // for clog >= 6 the index is wave-uniform (blocks of whole waves): a
+      // scalar load of the by-value argument (per-lane reads: ubench_small)
+      const unsigned i = (unsigned)row * ec.row + (k >> ec.clog);
+      mco = ec.p ? ec.p[i] : ec.v[ec.clog >= 6 ? __builtin_amdgcn_readfirstlane(i) : i];
+      addm = true;
+    }
+  }
   for (unsigned l = y * dst.per; l < (y + 1) * dst.per; l++) {
-    const uint64_t q = mc[dst.mod(l)].q;
-    dst.limb(l, logn)[k] = v >= 0 ? (uint64_t)v : q - (uint64_t)(-v);
+    const ModConst &m = mc[dst.mod(l)];
+    uint64_t r = v >= 0 ? (uint64_t)v : m.q - (uint64_t)(-v);
+    if (addm)
+      r = add_mod(r, lift_i64(mco, m), m.q);
+    dst.limb(l, logn)[k] = r;
   }
 }
 
-void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly)
+void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly, const EncCoef *ec)
 {
+  static const EncCoef none{};
   hipLaunchKernelGGL(sample_enc_kernel, dim3((G.n + TPB - 1) / TPB, npoly), dim3(TPB), 0, G.stream, dst, G.logn,
-                     G.key, stream, G.dev.mc);
+                     G.key, stream, G.dev.mc, ec ? *ec : none, ec ? 1 : 0);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1554,7 +1480,8 @@ __global__ void enc_batch_kernel(EncBatch bt, const uint64_t *vee, const uint64_
   const ModConst m = mc[blockIdx.y];
   const size_t o = ((size_t)blockIdx.y << logn) + i, w = (size_t)lvl << logn;
   const uint64_t *v = vee + 3 * e * w;
-  bt.c0[e][o] = add_mod(add_mod(v[w + o], mul_mod(v[o], pk0[o], m), m.q), bt.m[e][o], m.q);
+  const uint64_t c0 = add_mod(v[w + o], mul_mod(v[o], pk0[o], m), m.q);
+  bt.c0[e][o] = bt.m[e] ? add_mod(c0, bt.m[e][o], m.q) : c0;  // m == nullptr: already in e0 (EncCoef)
   bt.c1[e][o] = add_mod(v[2 * w + o], mul_mod(v[o], pk1[o], m), m.q);
 }
 
@@ -1897,22 +1824,25 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
 //   acc1 += pt_e * (sum_j D_j[perm_e k] evk_e,a[j])          (rotations)
 //   acc0 += pt_e * [P] x0[k], acc1 += pt_e * [P] x1[k]        (identity)
 // with the hoisted ModUp D of x; replaces one ks_inner launch per diagonal.
-// A block covers 32 coefficients of one basis slot with 8 diagonal lanes
-// (thread (c, g) sums diagonals g, g + 8, ...); the 8 partial sums meet in
-// LDS.  grid: (n / 32, nm), 256 threads.
-__global__ void __launch_bounds__(256) gemv_inner_kernel(GemvJobs jobs, unsigned logn, unsigned lvl, unsigned L,
+// A block covers 64 coefficients of one basis slot with 8 diagonal lanes, one
+// per wave (wave g sums diagonals g, g + 8, ...); the 8 partial sums meet in
+// LDS.  The diagonal index is wave-uniform, so its key / plaintext pointers and
+// Galois element come from the kernel arguments by scalar loads: per-lane reads
+// of by-value arguments took ~3.5 us more per launch (scripts/ubench_small).
+// grid: (n / 64, nm, jobs), 512 threads.
+__global__ void __launch_bounds__(512) gemv_inner_kernel(GemvJobs jobs, unsigned logn, unsigned lvl, unsigned L,
                                                           unsigned nm, unsigned nmod, unsigned ndig,
                                                           const ModConst *mc)
 {
-  __shared__ uint64_t part[2][8][32];
+  __shared__ uint64_t part[2][8][64];
   // blockIdx.z: the job (gemvs queued together run in one launch)
   const GemvJob &job = jobs.j[blockIdx.z];
   uint64_t *acc = job.acc;
   const uint64_t *D = job.D, *x0 = job.x0, *x1 = job.x1;
   const GemvDiags &dg = job.dg;
   const int accumulate = job.accumulate;
-  const unsigned c = threadIdx.x % 32, gl = threadIdx.x / 32;
-  const size_t k = (size_t)blockIdx.x * 32 + c;
+  const unsigned c = threadIdx.x % 64, gl = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  const size_t k = (size_t)blockIdx.x * 64 + c;
   const unsigned t = blockIdx.y;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mm = mc[m];
@@ -1961,7 +1891,7 @@ void k_gemv_inner_jobs(const GemvJobs &jobs, unsigned njobs, unsigned lvl)
   for (unsigned i = 0; i < njobs; i++)
     diags += jobs.j[i].dg.count;
   ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * diags * (ndig * nm + 2 * nm + 2 * lvl));
-  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 32, nm, njobs), dim3(256), 0, G.stream, jobs, G.logn, lvl, G.L,
+  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 64, nm, njobs), dim3(512), 0, G.stream, jobs, G.logn, lvl, G.L,
                      nm, G.nmod, ndig, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
@@ -2981,6 +2911,14 @@ __global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
   const unsigned t = blockIdx.x, p = blockIdx.y;
   const int th = threadIdx.x;
+  // X's words of this thread's outputs (the forward transform's last round
+  // leaves elements 8 th + k with the thread), requested before the
+  // conversion sum and the transform
+  const uint64_t *xt = X + p * x_pstride + ((size_t)t << LOGN);
+  uint64_t xk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    xk[k] = xt[8 * th + k];
   unsigned __int128 acc[8];
 #pragma unroll
   for (int k = 0; k < 8; k++)
@@ -2998,15 +2936,14 @@ __global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint
 #pragma unroll
   for (int k = 0; k < 8; k++)
     r[k] = redc128((uint64_t)(acc[k] >> 64), (uint64_t)acc[k], mc);
-  const uint64_t *xt = X + p * x_pstride + ((size_t)t << LOGN);
   uint64_t *dst = (p < half ? out + p * out_pstride : out2 + (p - half) * out_pstride) + ((size_t)t << LOGN);
   const uint64_t dinv = tab.dinv[t], dinvp = tab.dinvp[t];
   with_arith(mc.q, mt, LOGN, tw, [&](const auto &ar) {
     using A = std::decay_t<decltype(ar)>;
     small_fwd<LOGN>(
         ar, lds, [&](int k, int) { return A::load(r[k]); },
-        [&](int, int e, typename A::V a) {
-          dst[e] = mul_shoup(sub_mod(xt[e], ar.canon(a), mc.q), dinv, dinvp, mc.q);
+        [&](int k, int e, typename A::V a) {
+          dst[e] = mul_shoup(sub_mod(xk[k], ar.canon(a), mc.q), dinv, dinvp, mc.q);
         });
   });
 }

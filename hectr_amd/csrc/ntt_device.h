@@ -910,6 +910,111 @@ __device__ __forceinline__ void rows8_tile(const A &ar, const uint64_t *x, uint6
 }
 
 
+// ---------------------------------------------------------------------------
+// Whole-limb NTT rounds for n = 2^10 .. 2^12 (one block of n/8 threads per
+// limb, radix-8 register rounds; kernels.hip: ntt_small_kernel and the fused
+// small-N ModUp / ModDown / decode kernels).
+// ---------------------------------------------------------------------------
+// The rounds as device functions: the first loads and the last stores are the
+// caller's (load(k, i) -> V, store(k, i, V) for element i held in slot k).
+// The last inverse round and the first forward round both give thread th the
+// elements th + k n/8 (k < 8), so a caller can finish an inverse transform,
+// combine per element in registers and start a forward transform on the
+// result without an LDS pass (modup_small_kernel, moddown_small_kernel).
+template <int LOGN, class A, class LD, class ST>
+__device__ __forceinline__ void small_fwd(const A &ar, uint64_t *lds, LD &&load, ST &&store)
+{
+  using V = typename A::V;
+  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
+  const int th = threadIdx.x;
+  V a[8];
+#pragma unroll
+  for (int r = 0; r < FULL; r++) {
+    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = r ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
+    ar.template fwd<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 1);
+    if (r + 1 < FULL || REM) {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        lds[pos0 + k * d8] = A::bits(a[k]);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        store(k, pos0 + k * d8, a[k]);
+    }
+  }
+  if constexpr (REM > 0) {
+    // last REM stages (distances 2^(REM-1) .. 1): thread t owns 8
+    // consecutive elements = 8 / 2^REM groups
+    constexpr int EG = 1 << REM;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = A::unbits(lds[8 * th + k]);
+#pragma unroll
+    for (int j = 0; j < 8 / EG; j++) {
+      V g[EG];
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        g[e] = a[j * EG + e];
+      ar.template fwd<REM>(g, (uint64_t)n + 8 * th + EG * j, REM - 1);
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        store(j * EG + e, 8 * th + j * EG + e, g[e]);
+    }
+  }
+}
+
+template <int LOGN, class A, class LD, class ST>
+__device__ __forceinline__ void small_inv(const A &ar, uint64_t *lds, LD &&load, ST &&store)
+{
+  using V = typename A::V;
+  constexpr int n = 1 << LOGN, FULL = LOGN / 3, REM = LOGN % 3;
+  const int th = threadIdx.x;
+  V a[8];
+  if constexpr (REM > 0) {
+    constexpr int EG = 1 << REM;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = load(k, 8 * th + k);
+#pragma unroll
+    for (int j = 0; j < 8 / EG; j++) {
+      V g[EG];
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        g[e] = a[j * EG + e];
+      ar.template inv<REM>(g, (uint64_t)n + 8 * th + EG * j, 0);
+#pragma unroll
+      for (int e = 0; e < EG; e++)
+        lds[8 * th + j * EG + e] = A::bits(g[e]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int rr = 0; rr < FULL; rr++) {
+    const int r = FULL - 1 - rr;  // smallest distances first
+    const int d8 = n >> (3 * r + 3), pos0 = (th / d8) * 8 * d8 + th % d8;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      a[k] = (rr || REM) ? A::unbits(lds[pos0 + k * d8]) : load(k, pos0 + k * d8);
+    ar.template inv<3>(a, (uint64_t)n + pos0, LOGN - 3 * r - 3);
+    if (rr + 1 < FULL) {
+      __syncthreads();  // every group of this round has read its inputs
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        lds[pos0 + k * d8] = A::bits(a[k]);
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        store(k, pos0 + k * d8, a[k]);
+    }
+  }
+}
+
+
 __device__ __forceinline__ unsigned basis_mod(unsigned t, unsigned lvl, unsigned L)
 {
   return t < lvl ? t : L + (t - lvl);

@@ -507,6 +507,46 @@ def test_queued_encodes_mixed_slots(oracle, product, slot_set):
         assert np.array_equal(x, y), f"object {i} differs"
 
 
+@pytest.mark.parametrize("slot_set", [(16,) * 5, (16, 2, 512, 1), (1024,) * 5],
+                         ids=["kernel_args", "pinned_map", "upload"])
+def test_queued_encryptions_freed_plaintexts(oracle, product, slot_set):
+    """HECTR's step (reference src/ctr.c:466-480): encodes and encryptions
+    queued, then the plaintexts freed before anything ran.  A freed encode is
+    dropped and its encryption adds the plaintext's coefficients to e0 before
+    the transform (api.cpp drop_dead_encode, kernels.hip EncCoef); one
+    plaintext stays live, and a freed block is encoded into and encrypted
+    again while the dropped encode is still queued -- bit-exact vs the
+    oracle's sequential calls, and the decryptions within the CKKS tolerance."""
+    init_both(oracle, product, "ref")
+    rng = np.random.default_rng(8)
+    zs = [rng.uniform(-1, 1, s) + 1j * rng.uniform(-1, 1, s) for s in slot_set]
+    out = {}
+    for e in (oracle, product):
+        pk, sk, _, _ = keys(e, rot=False)
+        pts, cts = [], []
+        for z in zs:
+            pt = e.pt()
+            e.ecd_ex(pt, z, len(z), e.info.delta, e.L)
+            pts.append(pt)
+        for pt in pts:
+            ct = e.ct()
+            e.enc_pk(ct, pt, pk)
+            cts.append(ct)
+        for i, pt in enumerate(pts):
+            if i != 1:
+                e.free(pt)
+        pt2 = e.pt()  # may take a freed plaintext's block
+        e.ecd_ex(pt2, zs[0], len(zs[0]), e.info.delta, e.L)
+        ct2 = e.ct()
+        e.enc_pk(ct2, pt2, pk)
+        out[e.name] = [e.export(x) for x in cts + [pts[1], pt2, ct2]]
+        if e is product:
+            for z, ct in zip(zs, cts):
+                assert np.abs(e.decrypt(ct, sk, len(z)) - z).max() < 1e-6
+    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
+        assert np.array_equal(x, y), f"object {i} differs"
+
+
 @pytest.mark.parametrize("name", ["ref", "c1"])
 def test_plaintext_ops_rot0_and_queue_overflow(oracle, product, name):
     """he_add_pt (out != a: a queued copy the add then reads; and in place),
