@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <string>
@@ -181,6 +182,25 @@ struct PendEnc {
 static std::vector<PendEcd> g_pecd;
 static std::vector<int64_t> g_pcoef;  // 2 slots coefficient values per pending encode
 static std::vector<PendEnc> g_penc;
+
+// Speculative encryption noise.  HECTR encrypts its K = 5 states every control
+// step on consecutive RNG streams (src/ctr.c:471-475).  When a step ends in the
+// small-N he_dcd, the noise of the next K encryptions -- streams G.counter ..
+// G.counter + 3K - 1, sampled and transformed exactly as flush_pending would --
+// is launched behind the decode (the host waits for the decode only), so it
+// runs while the caller works on the host.  A later flush whose encryptions
+// take exactly those streams at that level uses it, and its combine
+// evaluates the plaintexts from their coefficients (k_enc_combine_m): the step
+// starts with the combine instead of sampling and transforms.
+struct SpecNoise {
+  uint64_t *buf = nullptr;  // [3k][lvl][n], NTT form (pool block, kept)
+  size_t words = 0;
+  uint64_t base = 0;  // first stream
+  unsigned k = 0, lvl = 0;
+  bool valid = false;
+};
+static SpecNoise g_spec;
+static unsigned g_spec_next_k = 0, g_spec_next_lvl = 0;  // the last flush's encryptions (one run)
 
 // he_gemv is queued the same way (at most two, run as one batch: the two
 // independent products of every control step of the caller, reference
@@ -403,6 +423,7 @@ static void set_seed_words(uint64_t seed)
     G.key.k[2 * i + 1] = (uint32_t)(x >> 32);
   }
   G.counter = 0;
+  g_spec.valid = false;  // noise of the old key
 }
 
 extern "C" void gpqhe_set_seed(uint64_t seed)
@@ -491,6 +512,71 @@ static unsigned env_u(const char *name, unsigned dflt)
   return (e && *e) ? (unsigned)strtoul(e, nullptr, 0) : dflt;
 }
 
+// GPQHE_HOSTPROF=1: host time spent inside each entry point the small-N
+// control step uses (outermost calls only) and between calls (the caller's
+// own work), printed to stderr by hectx_exit.  Measurement aid only.
+struct HostProfEntry {
+  double us = 0;
+  unsigned long calls = 0;
+};
+static std::map<std::string, HostProfEntry> g_hp;
+static double g_hp_outside = 0, g_hp_last = -1;
+static int g_hp_depth = 0;
+static double hp_now()
+{
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool hp_on()
+{
+  static const bool on = env_u("GPQHE_HOSTPROF", 0) != 0;
+  return on;
+}
+struct HpScope {
+  const char *name;
+  double t0 = 0;
+  bool top = false;
+  explicit HpScope(const char *nm) : name(nm)
+  {
+    if (!hp_on())
+      return;
+    top = g_hp_depth++ == 0;
+    if (top) {
+      t0 = hp_now();
+      if (g_hp_last >= 0)
+        g_hp_outside += t0 - g_hp_last;
+    }
+  }
+  ~HpScope()
+  {
+    if (!hp_on())
+      return;
+    g_hp_depth--;
+    if (top) {
+      g_hp_last = hp_now();
+      HostProfEntry &e = g_hp[name];
+      e.us += g_hp_last - t0;
+      e.calls++;
+    }
+  }
+};
+#define HPROF(nm) HpScope hp_scope_(nm)
+
+static void hp_report()
+{
+  if (!hp_on() || g_hp.empty())
+    return;
+  double in = 0;
+  for (auto &kv : g_hp)
+    in += kv.second.us;
+  fprintf(stderr, "[gpqhe hostprof] inside the library %.1f us, outside (caller) %.1f us\n", in, g_hp_outside);
+  for (auto &kv : g_hp)
+    fprintf(stderr, "[gpqhe hostprof] %-12s %8lu calls %10.1f us %8.2f us/call\n", kv.first.c_str(), kv.second.calls,
+            kv.second.us, kv.second.us / (double)kv.second.calls);
+  g_hp.clear();
+  g_hp_outside = 0;
+  g_hp_last = -1;
+}
+
 extern "C" void hectx_init(unsigned int logn, MPI q, unsigned int slots, uint64_t Delta)
 {
   gpqhe_params_t p;
@@ -525,10 +611,13 @@ extern "C" void hectx_exit(void)
 {
   if (!G.init)
     return;
+  hp_report();
   check_ctx();
   HIP_CHECK(hipStreamSynchronize(G.stream));
   gemv_cache_clear();
   tables_free();
+  g_spec = SpecNoise{};  // its block goes with the pool
+  g_spec_next_k = 0;
   pool_release_all();
   stage_release();
   G.init = false;
@@ -576,10 +665,26 @@ extern "C" void he_alloc_pk(he_pk_t *pk) { obj_alloc(pk, 2, G.L); }
 extern "C" void he_free_pk(he_pk_t *pk) { obj_free(pk); }
 extern "C" void he_alloc_sk(poly_mpi_t *sk) { obj_alloc(sk, 1, G.nmod); }
 extern "C" void he_free_sk(poly_mpi_t *sk) { obj_free(sk); }
-extern "C" void he_alloc_ct(he_ct_t *ct) { obj_alloc(ct, 2, G.L); }
-extern "C" void he_free_ct(he_ct_t *ct) { obj_free(ct); }
-extern "C" void he_alloc_pt(he_pt_t *pt) { obj_alloc(pt, 1, G.nmod); }
-extern "C" void he_free_pt(he_pt_t *pt) { obj_free(pt); }
+extern "C" void he_alloc_ct(he_ct_t *ct)
+{
+  HPROF("alloc_ct");
+  obj_alloc(ct, 2, G.L);
+}
+extern "C" void he_free_ct(he_ct_t *ct)
+{
+  HPROF("free_ct");
+  obj_free(ct);
+}
+extern "C" void he_alloc_pt(he_pt_t *pt)
+{
+  HPROF("alloc_pt");
+  obj_alloc(pt, 1, G.nmod);
+}
+extern "C" void he_free_pt(he_pt_t *pt)
+{
+  HPROF("free_pt");
+  obj_free(pt);
+}
 
 extern "C" void he_alloc_evk(he_evk_t *evk)
 {
@@ -828,6 +933,50 @@ static void flush_pending()
     unsigned mods[GPQHE_MAXMOD];
     for (unsigned l = 0; l < lvl; l++)
       mods[l] = l;
+    EncBatch b{};
+    for (unsigned e = 0; e < k; e++) {
+      b.c0[e] = enc[i0 + e].c0;
+      b.c1[e] = enc[i0 + e].c1;
+      b.m[e] = enc[i0 + e].ecd >= 0 ? nullptr : enc[i0 + e].m;
+    }
+    if (i0 == 0 && i1 == enc.size()) {
+      g_spec_next_k = k;
+      g_spec_next_lvl = lvl;
+    } else {
+      g_spec_next_k = 0;
+    }
+    // the speculative noise of exactly these streams: only the combine runs,
+    // with the queued plaintexts evaluated from their coefficients
+    const uint64_t off = (enc[i0].stream - g_spec.base) / 3;
+    unsigned mrows = 0;
+    for (unsigned e = 0; e < k; e++)
+      mrows += enc[i0 + e].ecd >= 0;
+    if (g_spec.valid && lvl == g_spec.lvl && enc[i0].stream >= g_spec.base &&
+        (enc[i0].stream - g_spec.base) % 3 == 0 && off + k <= g_spec.k && row >= 4 && row <= EncM::MAXROW &&
+        (size_t)mrows * lvl * row <= EncM::MAX) {
+      EncM em{};
+      em.row = (uint32_t)row;
+      em.clog = clog;
+      unsigned r = 0;
+      for (unsigned e = 0; e < k; e++) {
+        em.row_of[e] = -1;
+        const int ei = enc[i0 + e].ecd;
+        if (ei < 0)
+          continue;
+        for (unsigned l = 0; l < lvl; l++) {
+          const uint64_t q = G.q[l];
+          for (size_t j = 0; j < row; j++) {
+            const int64_t c = coef[(size_t)ei * row + j];
+            const uint64_t a = c >= 0 ? (uint64_t)c % q : (q - (uint64_t)(-(c + 1)) % q - 1) % q;
+            em.v[((size_t)r * lvl + l) * row + j] = a;
+          }
+        }
+        em.row_of[e] = (int32_t)r++;
+      }
+      k_enc_combine_m(b, em, k, g_spec.buf + off * 3 * w, enc[i0].pk0, enc[i0].pk1, lvl);
+      i0 = i1;
+      continue;
+    }
     // plaintexts that are queued encodes join e0 as coefficients (EncCoef):
     // the combine then reads no NTT-form plaintext
     EncCoef ec{};
@@ -852,12 +1001,6 @@ static void flush_pending()
     LimbSet s = limbset(vee.p, mods, lvl, 3 * k, w);
     k_sample_enc(s, enc[i0].stream, 3 * k, nrows ? &ec : nullptr);
     k_ntt(s, false);
-    EncBatch b{};
-    for (unsigned e = 0; e < k; e++) {
-      b.c0[e] = enc[i0 + e].c0;
-      b.c1[e] = enc[i0 + e].c1;
-      b.m[e] = enc[i0 + e].ecd >= 0 ? nullptr : enc[i0 + e].m;
-    }
     k_enc_combine_batch(b, k, vee.p, enc[i0].pk0, enc[i0].pk1, lvl);
     i0 = i1;
   }
@@ -885,6 +1028,7 @@ static void encode_limbs(uint64_t *dst, const double *z, unsigned s, double scal
 extern "C" void he_ecd_ex(he_pt_t *pt, const gpqhe_complex_t z[], unsigned int slots, double scale,
                           unsigned int nlimbs)
 {
+  HPROF("ecd");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   if (!defer_ok(slots))
@@ -939,8 +1083,41 @@ static void *zpin(size_t bytes)
   return dz;
 }
 
+// After the small-N decode (he_dcd_ex): record the decode's end, then launch
+// the next step's encryption noise (SpecNoise) if the last flush had one run
+// of encryptions.  True if launched (the caller then waits on g_dcd_ev).
+static hipEvent_t g_dcd_ev = nullptr;
+static bool spec_launch()
+{
+  static const bool on = env_u("GPQHE_SPEC", 1) != 0;
+  const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
+  if (!on || !k || !lvl || k > GPQHE_MAXGRP || !defer_ok(0))
+    return false;
+  if (!g_dcd_ev)
+    HIP_CHECK(hipEventCreateWithFlags(&g_dcd_ev, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(g_dcd_ev, G.stream));
+  const size_t w = (size_t)lvl << G.logn, words = 3 * (size_t)k * w;
+  if (g_spec.words != words) {
+    pool_free(g_spec.buf);  // stream-ordered: its last reader was launched before
+    g_spec.buf = (uint64_t *)pool_alloc(words * 8);
+    g_spec.words = words;
+  }
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned l = 0; l < lvl; l++)
+    mods[l] = l;
+  LimbSet s = limbset(g_spec.buf, mods, lvl, 3 * k, w);
+  k_sample_enc(s, G.counter, 3 * k);
+  k_ntt(s, false);
+  g_spec.base = G.counter;
+  g_spec.k = k;
+  g_spec.lvl = lvl;
+  g_spec.valid = true;
+  return true;
+}
+
 extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
 {
+  HPROF("dcd");
   const size_t zb = (size_t)slots * 16;
   if (G.init && defer_ok(0) && slots && !(slots & (slots - 1)) && slots <= GPQHE_DCD_ONEPASS &&
       slots <= G.n / 2 && !(pt->flags & GPQHE_F_COEFF) && pt->nlimbs >= 1 && pt->nlimbs <= 2) {
@@ -959,7 +1136,11 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     const EwProg p = g_pew;
     g_pew.count = 0;
     k_ew_decode(p, zd, pt->data, pt->nlimbs, slots, pt->scale, c.p);
-    HIP_CHECK(hipStreamSynchronize(G.stream));
+    if (spec_launch()) {
+      HIP_CHECK(hipEventSynchronize(g_dcd_ev));  // the decode, not the noise behind it
+    } else {
+      HIP_CHECK(hipStreamSynchronize(G.stream));
+    }
     memcpy(z, g_zpin, zb);
     return;
   }
@@ -995,6 +1176,7 @@ extern "C" void he_dcd(gpqhe_complex_t z[], const he_pt_t *pt)
 
 extern "C" void he_enc_pk(he_ct_t *ct, const he_pt_t *pt, const he_pk_t *pk)
 {
+  HPROF("enc_pk");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   const unsigned lvl = pt->nlimbs;
@@ -1084,6 +1266,7 @@ static void ew_push(uint32_t kind, uint64_t *out, const uint64_t *a, const uint6
 
 extern "C" void he_dec(he_pt_t *pt, const he_ct_t *ct, const poly_mpi_t *sk)
 {
+  HPROF("dec");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   if (ew_defer(1)) {
@@ -1128,11 +1311,20 @@ static void addsub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b, int op)
   out->flags = 0;
 }
 
-extern "C" void he_add(he_ct_t *out, const he_ct_t *a, const he_ct_t *b) { addsub(out, a, b, 0); }
-extern "C" void he_sub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b) { addsub(out, a, b, 1); }
+extern "C" void he_add(he_ct_t *out, const he_ct_t *a, const he_ct_t *b)
+{
+  HPROF("add");
+  addsub(out, a, b, 0);
+}
+extern "C" void he_sub(he_ct_t *out, const he_ct_t *a, const he_ct_t *b)
+{
+  HPROF("sub");
+  addsub(out, a, b, 1);
+}
 
 extern "C" void he_neg(he_ct_t *ct)
 {
+  HPROF("neg");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   if (ew_defer(2)) {
@@ -1146,6 +1338,7 @@ extern "C" void he_neg(he_ct_t *ct)
 
 extern "C" void he_copy_ct(he_ct_t *dst, const he_ct_t *src)
 {
+  HPROF("copy_ct");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   if (dst == src)
@@ -1166,6 +1359,7 @@ extern "C" void he_copy_ct(he_ct_t *dst, const he_ct_t *src)
 
 extern "C" void he_moddown(he_ct_t *ct)
 {
+  HPROF("moddown");
   // bookkeeping only (queued work captured its levels): no flush
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
@@ -1505,6 +1699,7 @@ static void gemv_now(he_ct_t *y, const double *Md, const he_ct_t *x, const he_ev
 
 extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
 {
+  HPROF("gemv");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
   flush_ew();  // x may be a queued difference

@@ -322,6 +322,19 @@ struct EncBatch {
 };
 void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, const uint64_t *pk0,
                          const uint64_t *pk1, unsigned lvl);
+// The same combine for plaintexts given by coefficients: encryption e with
+// row_of[e] >= 0 adds m in NTT form evaluated from its `row` coefficient
+// values (value j = coefficient j 2^clog; limb l's values, reduced mod q_l,
+// at v + (row_of[e] lvl + l) row); the others add b.m[e] if set.  n <= 2^12,
+// row a power of two in [4, MAXROW].
+struct EncM {
+  static constexpr unsigned MAX = 320, MAXROW = 64;
+  uint64_t v[MAX];
+  int32_t row_of[GPQHE_MAXGRP];
+  uint32_t row, clog;
+};
+void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
+                     const uint64_t *pk1, unsigned lvl);
 void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,
                       unsigned lvl);
 void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *sprime,

@@ -1493,6 +1493,67 @@ void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, con
   HIP_CHECK(hipGetLastError());
 }
 
+// The combine with m evaluated in NTT form from its coefficients: output k
+// holds m(psi^(2 brev(k) + 1)) = sum_j r_j y^j with y = psi^((2 brev(k) + 1)
+// 2^clog) (value j is coefficient j 2^clog), psi^e read as tw[brev(e mod n)]
+// and negated for e >= n (psi^n = -1).  The noise can then be sampled and
+// transformed before the plaintext exists (api.cpp: the speculative noise of
+// the small-N step).  Four lanes share an output: lane b sums the terms
+// j = 4a + b by Horner's rule in z = y^4 and multiplies by y^b, and the four
+// meet by lane shuffles -- a quarter of the serial chain of one lane per
+// output; each step's four values are read with uniform (scalar) loads of the
+// by-value argument, and the lane picks its own.  Lane 0 of the four writes
+// c0, lane 1 c1.  Every value is canonical, so the residues equal those of
+// NTT(m) added by enc_batch_kernel.
+__global__ void enc_batch_m_kernel(EncBatch bt, EncM em, const uint64_t *vee, const uint64_t *pk0,
+                                   const uint64_t *pk1, unsigned logn, unsigned lvl, const ModConst *mc,
+                                   const uint64_t *tw)
+{
+  const unsigned n = 1u << logn;
+  const unsigned g = blockIdx.x * blockDim.x + threadIdx.x, i = g >> 2, b = g & 3;
+  if (i >= n)
+    return;
+  const unsigned l = blockIdx.y, e = blockIdx.z;
+  const ModConst m = mc[l];
+  const size_t o = ((size_t)l << logn) + i, w = (size_t)lvl << logn;
+  const uint64_t *v = vee + 3 * e * w;
+  uint64_t mh = 0;
+  const int r = em.row_of[e];
+  if (r >= 0) {  // (uniform)
+    const uint64_t *cv = em.v + ((size_t)r * lvl + l) * em.row;
+    const unsigned br = __brev(i) >> (32 - logn);
+    const unsigned ex = ((2 * br + 1) << em.clog) & (2 * n - 1);
+    const uint64_t y0 = tw[(size_t)l * n + (__brev(ex & (n - 1)) >> (32 - logn))];
+    const uint64_t y = ex >= n ? m.q - y0 : y0;
+    const uint64_t y2 = mul_mod(y, y, m), y4 = mul_mod(y2, y2, m);
+    uint64_t acc = 0;
+    for (int a = (int)em.row / 4 - 1; a >= 0; a--) {
+      const uint64_t c0v = cv[4 * a], c1v = cv[4 * a + 1], c2v = cv[4 * a + 2], c3v = cv[4 * a + 3];
+      acc = add_mod(mul_mod(acc, y4, m), b == 0 ? c0v : b == 1 ? c1v : b == 2 ? c2v : c3v, m.q);
+    }
+    if (b)
+      acc = mul_mod(acc, b == 1 ? y : b == 2 ? y2 : mul_mod(y2, y, m), m);
+    mh = add_mod(acc, __shfl_xor(acc, 1), m.q);
+    mh = add_mod(mh, __shfl_xor(mh, 2), m.q);
+  } else if (bt.m[e] && b == 0) {
+    mh = bt.m[e][o];
+  }
+  if (b == 0)
+    bt.c0[e][o] = add_mod(add_mod(v[w + o], mul_mod(v[o], pk0[o], m), m.q), mh, m.q);
+  else if (b == 1)
+    bt.c1[e][o] = add_mod(v[2 * w + o], mul_mod(v[o], pk1[o], m), m.q);
+}
+
+void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
+                     const uint64_t *pk1, unsigned lvl)
+{
+  if (G.logn > 12 || em.row < 4 || em.row > EncM::MAXROW || (em.row & (em.row - 1)))
+    gpqhe_die("k_enc_combine_m: %u values per row at n = %u", em.row, G.n);
+  hipLaunchKernelGGL(enc_batch_m_kernel, dim3((4 * G.n + TPB - 1) / TPB, lvl, k), dim3(TPB), 0, G.stream, b, em, vee,
+                     pk0, pk1, G.logn, lvl, G.dev.mc, G.dev.tw);
+  HIP_CHECK(hipGetLastError());
+}
+
 // c0 = e - a s + m
 __global__ void enc_sk_kernel(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s,
                               const uint64_t *mp, unsigned logn, const ModConst *mc)

@@ -547,6 +547,54 @@ def test_queued_encryptions_freed_plaintexts(oracle, product, slot_set):
         assert np.array_equal(x, y), f"object {i} differs"
 
 
+def test_speculative_encryption_noise(oracle, product):
+    """The small-N step's speculative noise (api.cpp SpecNoise): after each
+    he_dcd the noise of the next step's encryptions is sampled ahead, and a
+    flush whose encryptions take exactly those streams only runs the combine,
+    evaluating the plaintexts from their coefficients (k_enc_combine_m).
+    Steps of 5 encryptions (HECTR's), then 3 (a prefix of the speculated
+    streams), 6 (more than speculated), one of a live plaintext, an
+    encryption at a lower level, and a reseed between steps -- every
+    ciphertext bit-exact vs the oracle's sequential calls."""
+    init_both(oracle, product, "ref")
+    rng = np.random.default_rng(9)
+    plan = [5, 5, 3, 6, "live", "lvl1", "reseed", 5, 5]
+    zs = [[rng.uniform(-1, 1, oracle.slots) + 0j for _ in range(6)] for _ in plan]
+    out = {}
+    for e in (oracle, product):
+        pk, sk, _, _ = keys(e, rot=False)
+        res = []
+        for step, (kind, zz) in enumerate(zip(plan, zs)):
+            if kind == "reseed":
+                e.set_seed(77)
+                continue
+            cnt = kind if isinstance(kind, int) else 2
+            lvl = 1 if kind == "lvl1" else e.L
+            pts, cts = [], []
+            for z in zz[:cnt]:
+                pt = e.pt()
+                e.ecd_ex(pt, z, e.slots, e.info.delta, lvl)
+                pts.append(pt)
+            for pt in pts:
+                ct = e.ct()
+                e.enc_pk(ct, pt, pk)
+                cts.append(ct)
+            if kind == "live":
+                res.append(e.export(pts[0]))
+            for pt in pts:
+                e.free(pt)
+            d = e.ct()
+            e.sub(d, cts[0], cts[1])
+            res += [e.export(x) for x in cts + [d]]
+            res.append(e.decrypt(d, sk))  # he_dcd: the next step's noise is launched behind it
+            for x in cts + [d]:
+                e.free(x)
+        out[e.name] = res
+    assert len(out["oracle"]) == len(out["product"])
+    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
+        assert np.array_equal(x, y), f"object {i} differs"
+
+
 @pytest.mark.parametrize("name", ["ref", "c1"])
 def test_plaintext_ops_rot0_and_queue_overflow(oracle, product, name):
     """he_add_pt (out != a: a queued copy the add then reads; and in place),
