@@ -201,6 +201,48 @@ struct SpecNoise {
 };
 static SpecNoise g_spec;
 static unsigned g_spec_next_k = 0, g_spec_next_lvl = 0;  // the last flush's encryptions (one run)
+static uint64_t g_step_base = 0;                          // their first stream
+
+// Speculative ModUp.  The c1 of a fresh encryption, v pk1 + e1, does not
+// depend on the plaintext, and HECTR's he_gemv inputs are differences of two
+// fresh encryptions (src/hempc.c:253-259).  The queued small-N calls record
+// how each c1 poly was made (C1Prov: an encryption's stream, or the he_sub of
+// two of them); when a step's gemv inputs were such differences, the next
+// step's he_dcd also forms the same differences from the speculative noise
+// and runs their ModUp, and a he_gemv whose input c1 has exactly that
+// provenance (same streams, public key and level) takes the precomputed
+// digits.  Any other write clears the record (check_ctx, non-queued writers),
+// so a match always names the same values.
+struct C1Prov {
+  uint64_t sa, sb;  // streams: the encryption's (sb unused), or a - b
+  const uint64_t *pk1;
+  unsigned lvl;
+  bool sub;
+};
+static std::unordered_map<const uint64_t *, C1Prov> g_prov;
+struct SpecPat {
+  unsigned oa, ob;  // encryption offsets within the step's run
+};
+static std::vector<SpecPat> g_spec_pats_next;  // the last step's gemv inputs
+static const uint64_t *g_spec_pk1_next = nullptr;
+struct SpecModup {
+  uint64_t *D = nullptr;  // [np][ndig][nm][n]
+  size_t dwords = 0;
+  std::vector<SpecPat> pats;
+  uint64_t base = 0;
+  const uint64_t *pk1 = nullptr;
+  unsigned lvl = 0;
+  bool valid = false;
+};
+static SpecModup g_smu;
+
+static void prov_forget(const void *obj_data, size_t pstride_words)
+{
+  if (g_prov.empty() || !obj_data)
+    return;
+  g_prov.erase((const uint64_t *)obj_data);
+  g_prov.erase((const uint64_t *)obj_data + pstride_words);
+}
 
 // he_gemv is queued the same way (at most two, run as one batch: the two
 // independent products of every control step of the caller, reference
@@ -214,6 +256,7 @@ struct PendGemv {
   const void *xdata;
   unsigned lvl;
   std::vector<GemvDiags> dgs;  // launches of up to GemvDiags::MAX diagonals; empty: all-zero matrix
+  const uint64_t *dspec = nullptr;  // x1's ModUp digits, precomputed (SpecModup), or null
 };
 static std::vector<PendGemv> g_pgemv;
 
@@ -242,6 +285,9 @@ static void check_ctx()
 {
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
+  // a non-queued entry point: it may write any object (C1Prov)
+  g_prov.clear();
+  g_smu.valid = false;
   flush_ew();
   if (!g_pgemv.empty())
     flush_gemvs();
@@ -306,6 +352,7 @@ static void obj_alloc(void *vo, unsigned npoly, unsigned cap)
   // No zero fill: a fresh object has nlimbs = 0, and every read of an object
   // is bounded by its nlimbs, so its payload is written before it is read.
   o->data = (uint64_t *)pool_alloc(bytes);
+  prov_forget(o->data, (size_t)cap << G.logn);
 }
 
 // Freeing the target of a queued encode that no other queued work reads
@@ -337,8 +384,15 @@ static void obj_free(void *vo)
   if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty()) && !drop_dead_encode(OB(vo)->data))
     check_ctx();
   he_ct_t *o = OB(vo);
-  if (o->data && G.init)
+  if (o->data && G.init) {
+    prov_forget(o->data, (size_t)o->cap << G.logn);
+    const uint64_t *lo = o->data, *hi = o->data + ((size_t)o->npoly * o->cap << G.logn);
+    if (g_smu.pk1 >= lo && g_smu.pk1 < hi)
+      g_smu.valid = false;  // the speculative ModUp's public key
+    if (g_spec_pk1_next >= lo && g_spec_pk1_next < hi)
+      g_spec_pats_next.clear();
     pool_free(o->data);
+  }
   memset(o, 0, sizeof(*o));
 }
 
@@ -424,6 +478,7 @@ static void set_seed_words(uint64_t seed)
   }
   G.counter = 0;
   g_spec.valid = false;  // noise of the old key
+  g_smu.valid = false;
 }
 
 extern "C" void gpqhe_set_seed(uint64_t seed)
@@ -616,8 +671,12 @@ extern "C" void hectx_exit(void)
   HIP_CHECK(hipStreamSynchronize(G.stream));
   gemv_cache_clear();
   tables_free();
-  g_spec = SpecNoise{};  // its block goes with the pool
+  g_spec = SpecNoise{};  // its blocks go with the pool
   g_spec_next_k = 0;
+  g_smu = SpecModup{};
+  g_prov.clear();
+  g_spec_pats_next.clear();
+  g_spec_pk1_next = nullptr;
   pool_release_all();
   stage_release();
   G.init = false;
@@ -912,8 +971,10 @@ static void flush_pending()
       mods[l] = l;
     LimbSet ls = limbset(nullptr, mods, ecd[i0].lvl, (unsigned)(i1 - i0), 0);
     ls.ngp = (uint32_t)(i1 - i0);
-    for (size_t i = i0; i < i1; i++)
+    for (size_t i = i0; i < i1; i++) {
       ls.gp[i - i0] = ecd[i].dst;
+      g_prov.erase(ecd[i].dst);
+    }
     // up to CoefArg::MAX values (HECTR's step: 5 x 32) in the kernel arguments
     if ((i1 - i0) * row <= CoefArg::MAX)
       k_lift_ntt_arg(ls, coef.data() + i0 * row, clog);
@@ -942,8 +1003,15 @@ static void flush_pending()
     if (i0 == 0 && i1 == enc.size()) {
       g_spec_next_k = k;
       g_spec_next_lvl = lvl;
+      g_step_base = enc[i0].stream;
     } else {
       g_spec_next_k = 0;
+    }
+    if (i0 == 0)
+      g_spec_pats_next.clear();  // a new step: its gemv inputs are recorded afresh
+    for (unsigned e = 0; e < k; e++) {
+      g_prov[enc[i0 + e].c1] = C1Prov{enc[i0 + e].stream, 0, enc[i0 + e].pk1, lvl, false};
+      g_prov.erase(enc[i0 + e].c0);
     }
     // the speculative noise of exactly these streams: only the combine runs,
     // with the queued plaintexts evaluated from their coefficients
@@ -1112,6 +1180,33 @@ static bool spec_launch()
   g_spec.k = k;
   g_spec.lvl = lvl;
   g_spec.valid = true;
+  // the gemv inputs of the last step, made from the same encryption slots of
+  // this noise: their c1 differences and ModUp (SpecModup)
+  g_smu.valid = false;
+  const std::vector<SpecPat> &pats = g_spec_pats_next;
+  bool ok = !pats.empty() && g_spec_pk1_next && lvl >= 2;
+  for (const SpecPat &p : pats)
+    ok &= p.oa < k && p.ob < k;
+  if (ok) {
+    const unsigned np = (unsigned)pats.size(), nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+    const size_t dw = (size_t)np * ndig * nm << G.logn;
+    if (g_smu.dwords != dw) {
+      pool_free(g_smu.D);
+      g_smu.D = (uint64_t *)pool_alloc(dw * 8);
+      g_smu.dwords = dw;
+    }
+    C1Diffs cd{};
+    for (unsigned i = 0; i < np; i++) {
+      cd.va[i] = g_spec.buf + (size_t)3 * pats[i].oa * w;
+      cd.vb[i] = g_spec.buf + (size_t)3 * pats[i].ob * w;
+    }
+    k_modup_ntt_diffs(g_smu.D, cd, np, (size_t)ndig * nm << G.logn, g_spec_pk1_next, lvl);
+    g_smu.pats = pats;
+    g_smu.base = g_spec.base;
+    g_smu.pk1 = g_spec_pk1_next;
+    g_smu.lvl = lvl;
+    g_smu.valid = true;
+  }
   return true;
 }
 
@@ -1262,6 +1357,22 @@ static void ew_push(uint32_t kind, uint64_t *out, const uint64_t *a, const uint6
                     unsigned lvl)
 {
   g_pew.op[g_pew.count++] = EwOp{out, a, b, sk, kind, lvl};
+  // out's provenance after this op (C1Prov): the difference of two fresh
+  // encryptions at their full level with one public key, or none
+  C1Prov d{};
+  bool known = false;
+  if (kind == EW_SUB && !g_prov.empty()) {
+    auto ia = g_prov.find(a), ib = g_prov.find(b);
+    if (ia != g_prov.end() && ib != g_prov.end() && !ia->second.sub && !ib->second.sub &&
+        ia->second.pk1 == ib->second.pk1 && ia->second.lvl == lvl && ib->second.lvl == lvl) {
+      d = C1Prov{ia->second.sa, ib->second.sa, ia->second.pk1, lvl, true};
+      known = true;
+    }
+  }
+  if (known)
+    g_prov[out] = d;
+  else if (!g_prov.empty())
+    g_prov.erase(out);
 }
 
 extern "C" void he_dec(he_pt_t *pt, const he_ct_t *ct, const poly_mpi_t *sk)
@@ -1615,11 +1726,25 @@ static void flush_gemvs()
   const unsigned k = (unsigned)q.size(), lvl = q[0].lvl;
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  Ws D((size_t)k * ndig * nm * n), acc((size_t)k * 2 * nm * n);
-  XPtrs x1{};
+  // ModUp of the inputs without precomputed digits (SpecModup), in one pass
+  const size_t dstride = (size_t)ndig * nm * n;
+  unsigned miss = 0;
   for (unsigned i = 0; i < k; i++)
-    x1.p[i] = q[i].x1;
-  k_modup_ntt(D.p, x1, k, (size_t)ndig * nm * n, lvl);
+    miss += !q[i].dspec;
+  Ws D((size_t)miss * dstride), acc((size_t)k * 2 * nm * n);
+  std::vector<const uint64_t *> Dp(k);
+  XPtrs x1{};
+  for (unsigned i = 0, m = 0; i < k; i++) {
+    if (q[i].dspec) {
+      Dp[i] = q[i].dspec;
+    } else {
+      x1.p[m] = q[i].x1;
+      Dp[i] = D.p + m++ * dstride;
+    }
+    prov_forget(q[i].y, q[i].ypstride);
+  }
+  if (miss)
+    k_modup_ntt(D.p, x1, miss, dstride, lvl);
   // every gemv with one launch's worth of diagonals: all in one launch
   bool one = k <= GemvJobs::MAX;
   for (unsigned i = 0; i < k; i++)
@@ -1627,15 +1752,14 @@ static void flush_gemvs()
   if (one) {
     GemvJobs jobs;
     for (unsigned i = 0; i < k; i++)
-      jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1,
-                          q[i].dgs[0], 0};
+      jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, Dp[i], q[i].x0, q[i].x1, q[i].dgs[0], 0};
     k_gemv_inner_jobs(jobs, k, lvl);
   } else {
     for (unsigned i = 0; i < k; i++) {
       uint64_t *a = acc.p + (size_t)i * 2 * nm * n;
       bool started = false;
       for (const GemvDiags &dg : q[i].dgs) {
-        k_gemv_inner(a, D.p + (size_t)i * ndig * nm * n, q[i].x0, q[i].x1, lvl, dg, started);
+        k_gemv_inner(a, Dp[i], q[i].x0, q[i].x1, lvl, dg, started);
         started = true;
       }
       if (!started)  // all-zero matrix
@@ -1652,6 +1776,7 @@ static void flush_gemvs()
 // launch that refers to cached diagonals runs before the cache is cleared.
 static void gemv_now(he_ct_t *y, const double *Md, const he_ct_t *x, const he_evk_t rk[], unsigned lvl)
 {
+  prov_forget(y->data, pstride(y));
   const unsigned s = G.slots, nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
   Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
@@ -1728,6 +1853,29 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
       flush_gemvs();
   }
   PendGemv pg{y->data, pstride(y), limb(x, 0, 0), limb(x, 1, 0), x->data, lvl, {}};
+  prov_forget(y->data, pstride(y));
+  // x's c1: the difference of two fresh encryptions of this step?  Then its
+  // ModUp may be precomputed (SpecModup), and the pattern is kept for the
+  // next step's speculation.
+  auto pv = g_prov.find(pg.x1);
+  if (pv != g_prov.end() && pv->second.sub && pv->second.lvl == lvl) {
+    const C1Prov &c = pv->second;
+    if (g_smu.valid && g_smu.lvl == lvl && g_smu.pk1 == c.pk1)
+      for (size_t i = 0; i < g_smu.pats.size(); i++)
+        if (g_smu.base + 3 * (uint64_t)g_smu.pats[i].oa == c.sa && g_smu.base + 3 * (uint64_t)g_smu.pats[i].ob == c.sb) {
+          const unsigned nmx = lvl + G.K, ndx = (lvl + G.alpha - 1) / G.alpha;
+          pg.dspec = g_smu.D + i * ((size_t)ndx * nmx << G.logn);
+          break;
+        }
+    const uint64_t span = 3 * (uint64_t)g_spec_next_k;
+    if (g_spec_next_k && lvl == g_spec_next_lvl && c.sa >= g_step_base && c.sb >= g_step_base &&
+        c.sa < g_step_base + span && c.sb < g_step_base + span && (c.sa - g_step_base) % 3 == 0 &&
+        (c.sb - g_step_base) % 3 == 0 && g_spec_pats_next.size() < XPtrs::MAX &&
+        (g_spec_pats_next.empty() || g_spec_pk1_next == c.pk1)) {
+      g_spec_pk1_next = c.pk1;
+      g_spec_pats_next.push_back({(unsigned)((c.sa - g_step_base) / 3), (unsigned)((c.sb - g_step_base) / 3)});
+    }
+  }
   const size_t mwords = 2 * (size_t)s * s;
   for (const GemvMat &gm : g_gemv_mats)
     if (gm.s == s && gm.lvl == lvl && !memcmp(gm.M.data(), Md, mwords * 8)) {

@@ -335,6 +335,15 @@ struct EncM {
 };
 void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
                      const uint64_t *pk1, unsigned lvl);
+// The c1 of the difference of two fresh encryptions without their plaintexts:
+// c1(a_i) - c1(b_i), c1(x) = v pk1 + e1 of the sampled noise (v, e0, e1) at
+// va[i] / vb[i] (NTT form, lvl limbs each).  k_modup_ntt_diffs: their ModUp,
+// each value formed at load (n <= 2^12).
+struct C1Diffs {
+  const uint64_t *va[GPQHE_MAXGRP], *vb[GPQHE_MAXGRP];
+};
+void k_modup_ntt_diffs(uint64_t *D, const C1Diffs &cd, unsigned np, size_t d_stride, const uint64_t *pk1,
+                       unsigned lvl);
 void k_enc_sk_combine(uint64_t *c0, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *m,
                       unsigned lvl);
 void k_evk_combine(uint64_t *b, const uint64_t *a, const uint64_t *e, const uint64_t *s, const uint64_t *sprime,

@@ -2820,10 +2820,14 @@ __global__ void down_combine_kernel(uint64_t *out, uint64_t *out2, unsigned half
 // Replaces copy + INTT + modup_kernel + NTT (four launches) with one; every
 // value equals theirs (canonical residues at each step).
 // grid: (nm, ndig, count), n / 8 threads.
-template <int LOGN>
+// DIFF: input p is not in memory but the c1 difference of two fresh
+// encryptions formed from their noise at load, (v_a pk1 + e1_a) - (v_b pk1 +
+// e1_b) as enc_batch_kernel and the queued he_sub form it (the speculative
+// ModUp of the small-N step, api.cpp SpecModup).
+template <int LOGN, bool DIFF>
 __global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1, size_t d_stride, unsigned lvl,
                                                            unsigned L, unsigned nm, Tw2 tw, UpTable tab,
-                                                           const ModConst *mcs)
+                                                           const ModConst *mcs, C1Diffs cd, const uint64_t *pk1)
 {
   constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
@@ -2833,10 +2837,24 @@ __global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1,
   const uint64_t *x = x1.p[p];
   uint64_t *out = D + p * d_stride + (((size_t)j * nm + t) << LOGN);
   const int th = threadIdx.x;
+  // input word e of limb ms
+  auto xin = [&](unsigned ms, int e, const ModConst &m) -> uint64_t {
+    const size_t o = ((size_t)ms << LOGN) + e;
+    if constexpr (DIFF) {
+      const size_t w = (size_t)lvl << LOGN;
+      const uint64_t *a = cd.va[p], *b = cd.vb[p];
+      const uint64_t ca = add_mod(a[2 * w + o], mul_mod(a[o], pk1[o], m), m.q);
+      const uint64_t cb = add_mod(b[2 * w + o], mul_mod(b[o], pk1[o], m), m.q);
+      return sub_mod(ca, cb, m.q);
+    } else {
+      return x[o];
+    }
+  };
   if (t >= lo && t < lo + na) {
+    const ModConst m = mcs[t];
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      out[th + k * (n / 8)] = x[((size_t)t << LOGN) + th + k * (n / 8)];
+      out[th + k * (n / 8)] = xin(t, th + k * (n / 8), m);
     return;
   }
   unsigned __int128 acc[8];
@@ -2847,14 +2865,13 @@ __global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1,
   for (unsigned i = 0; i < na; i++) {
     const unsigned ms = lo + i;
     const ModConst mc = mcs[ms];
-    const uint64_t *src = x + ((size_t)ms << LOGN);
     const uint64_t cw = cj[i * nm + t], yw = dg->y[i], ywp = dg->yp[i];
     if (i)
       __syncthreads();
     with_arith(mc.q, ms, LOGN, tw, [&](const auto &ar) {
       using A = std::decay_t<decltype(ar)>;
       small_inv<LOGN>(
-          ar, lds, [&](int, int e) { return A::load(src[e]); },
+          ar, lds, [&](int, int e) { return A::load(xin(ms, e, mc)); },
           [&](int k, int, typename A::V a) {
             const uint64_t y = mul_shoup(ar.mulc(a, mc.ninv, mc.ninvp), yw, ywp, mc.q);
             acc[k] += (unsigned __int128)y * cw;
@@ -3023,14 +3040,14 @@ void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, 
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(nm, ndig, count), dim3(n / 8), 0, G.stream, D, x1, d_stride, lvl, G.L, nm, tw,
-                         tab, G.dev.mc);
+                         tab, G.dev.mc, C1Diffs{}, (const uint64_t *)nullptr);
     };
     if (G.logn == 12)
-      go(modup_small_kernel<12>);
+      go(modup_small_kernel<12, false>);
     else if (G.logn == 11)
-      go(modup_small_kernel<11>);
+      go(modup_small_kernel<11, false>);
     else
-      go(modup_small_kernel<10>);
+      go(modup_small_kernel<10, false>);
     HIP_CHECK(hipGetLastError());
     return;
   }
@@ -3056,6 +3073,30 @@ void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, 
   basis_qp(lvl, mods);
   k_ntt(limbs(D, mods, nm, count * ndig, (size_t)nm * n), false);
   pool_free(c1c);
+}
+
+// k_modup_ntt of np c1 differences formed from encryption noise (C1Diffs) at
+// load, n <= 2^12.
+void k_modup_ntt_diffs(uint64_t *D, const C1Diffs &cd, unsigned np, size_t d_stride, const uint64_t *pk1,
+                       unsigned lvl)
+{
+  UpTable &tab = up_table(lvl);
+  const unsigned nm = tab.nm, ndig = tab.ndig, n = G.n;
+  if (G.logn < 10 || G.logn > 12 || !np || np > GPQHE_MAXGRP)
+    gpqhe_die("k_modup_ntt_diffs: %u inputs at n = %u", np, n);
+  ProfScope ps(KC_MODUP_SMALL, 8.0 * n * np * ((double)ndig * lvl + ndig * nm));
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nm, ndig, np), dim3(n / 8), 0, G.stream, D, XPtrs{}, d_stride, lvl, G.L, nm, tw, tab,
+                       G.dev.mc, cd, pk1);
+  };
+  if (G.logn == 12)
+    go(modup_small_kernel<12, true>);
+  else if (G.logn == 11)
+    go(modup_small_kernel<11, true>);
+  else
+    go(modup_small_kernel<10, true>);
+  HIP_CHECK(hipGetLastError());
 }
 
 // X: npoly polynomials over basis_qp(lvl) (NTT domain, nm limbs each, stride
