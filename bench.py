@@ -23,7 +23,8 @@ Also reported (rank 0):
                   and the PMC traffic of the pipeline beside it;
   op_roofline   - the whole op against its algorithmic bytes;
   value_60bit   - the same op with the conventional 60-bit q0 / special primes;
-  config5       - n=2^17, L=12 (dnum 3, K 4), per GPU and aggregate;
+  config5       - n=2^17, L=12 (dnum 3, K 4), per GPU and aggregate, at the
+                  headline's prime sizes and at the 60-bit ones;
   ntt_roundtrip - config 2 (1024 polys, forward + inverse, identity checked);
   cstr          - config 4, the encrypted CSTR-MPC loop;
   cpu_baseline  - the CPU restatement (oracle/, "port") on this host.
@@ -585,21 +586,35 @@ def main():
         barrier()
 
     if not args.no_c5:
-        # config 5: n = 2^17, L = 12 (dnum 3, K 4, conventional primes), each
-        # rank its own shard of the global batch
-        c5 = MulBatch(stream, 17, 12, 3, 60, 60, 4, args.c5_batch, rank * args.c5_batch, 2000 + rank)
-        c5.eng.lib.gpqhe_set_streams(args.streams)
+        # config 5: n = 2^17, L = 12 (dnum 3, K 4), each rank its own shard of
+        # the global batch; the headline's prime sizes (q0 and P of
+        # --q0-bits / --p-bits: every modulus below 2^51) and the conventional
+        # 60-bit q0 / P beside them, same harness
         steps5 = max(2, args.steps // 2)
-        t = hdist.max_over_ranks(timed(c5.step, steps5, 1, c5.eng.sync, barrier), device=red_dev)
+
+        def c5_leg(q0_bits, p_bits):
+            c5 = MulBatch(stream, 17, 12, 3, q0_bits, p_bits, 4, args.c5_batch, rank * args.c5_batch, 2000 + rank)
+            c5.eng.lib.gpqhe_set_streams(args.streams)
+            t = hdist.max_over_ranks(timed(c5.step, steps5, 1, c5.eng.sync, barrier), device=red_dev)
+            leg = None
+            if rank == 0:
+                v = world * args.c5_batch * steps5 / t
+                leg = {"workload": f"ct x ct mult + relin + rescale, N=2^17, L=12, K=4, dnum=3, "
+                                   f"primes {q0_bits}/50/{p_bits} bits, batch={args.c5_batch} pairs per GPU",
+                       "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "ct-mult/s",
+                       "steps": steps5, "ms_per_step": 1e3 * t / steps5,
+                       "op_roofline_frac": c5.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
+            c5.close()
+            barrier()
+            return leg
+
+        main5 = c5_leg(args.q0_bits, args.p_bits)
+        alt5 = c5_leg(args.alt_bits, args.alt_bits) if args.alt_bits and args.alt_bits != args.q0_bits else None
         if rank == 0:
-            v = world * args.c5_batch * steps5 / t
-            result["config5"] = {"workload": f"ct x ct mult + relin + rescale, N=2^17, L=12, K=4, dnum=3, "
-                                             f"primes 60/50/60 bits, batch={args.c5_batch} pairs per GPU",
-                                 "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "ct-mult/s",
-                                 "steps": steps5, "ms_per_step": 1e3 * t / steps5,
-                                 "op_roofline_frac": c5.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
-        c5.close()
-        barrier()
+            result["config5"] = main5
+            if alt5:
+                main5["value_60bit"] = alt5["value"]
+                main5["alt_primes"] = alt5
 
     if rank == 0 and world == 1 and not args.no_cstr:
         result["cstr"] = cstr_loop(args.cstr_steps)

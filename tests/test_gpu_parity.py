@@ -36,6 +36,9 @@ PARAMS = {
     "bench_d2": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=60, qi_bits=50,
                                 p_bits=60)),
     "c5": ("params", dict(logn=17, nlimbs=12, nspecial=4, dnum=3, slots=64, q0_bits=60, qi_bits=50, p_bits=60)),
+    # config 5 at the headline's prime sizes (every modulus below 2^51: the
+    # all-FP64 three-digit split key switch), bench.py's config5 value
+    "c5f": ("params", dict(logn=17, nlimbs=12, nspecial=4, dnum=3, slots=64, q0_bits=51, qi_bits=50, p_bits=51)),
     "bench51": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50,
                                p_bits=51)),
     "c17": ("params", dict(logn=17, nlimbs=8, nspecial=4, dnum=2, slots=64, q0_bits=51, qi_bits=50, p_bits=51)),
@@ -146,7 +149,7 @@ def test_evaluation_ops(oracle, product, name):
         assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
 
 
-@pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c14", "c15"])
+@pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c5f", "c14", "c15"])
 @pytest.mark.parametrize("npolys", [4, 24])
 def test_ntt_batch_bitexact(oracle, product, name, npolys):
     """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain: forward, then
@@ -235,7 +238,7 @@ def mul_batch_both(oracle, product, name, cnt, lvl=None, seeds=(1, 2)):
     return out_o, got
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c17", "c14", "c15", "a5"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c5f", "c17", "c14", "c15", "a5"])
 def test_mul_rescale_batch_bitexact(oracle, product, name):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 through the streaming inner
     product, the bench's dnum=2/K=4 with 60-bit and with < 2^51 primes), the
@@ -247,7 +250,8 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
 
 @pytest.mark.parametrize("name,cnt,chunk", [("bench51", 17, None), ("bench51", 24, None), ("bench_d2", 17, None),
                                             ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None),
-                                            ("c5", 17, None), ("c5", 64, None), ("c15", 17, None)])
+                                            ("c5", 17, None), ("c5", 64, None), ("c5f", 17, None), ("c5f", 64, None),
+                                            ("c15", 17, None)])
 def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
     """The headline shape (bench.py): n=2^16, L=8,
     dnum=2, K=4 on 17 and 24 pairs (the split key switch's pair ranges of
@@ -258,7 +262,8 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     chunks of the 8 GiB workspace, about 3 pairs per quarter), every output
     residue compared with the oracle.  Also 17 pairs of config 5 (n=2^17, L=12,
     the three-digit split key switch), config 5's own bench shape (64 pairs per
-    GPU, bench.py's c5 leg: its pair ranges and member split) and 17 of c15
+    GPU, bench.py's c5 leg: its pair ranges and member split), both on the
+    60-bit q0/P set and on the headline's all-FP64 prime sizes (c5f), and 17 of c15
     (integer moduli: two pair streams per workgroup)."""
     if chunk:
         monkeypatch.setenv("GPQHE_CHUNK", str(chunk))
