@@ -257,6 +257,9 @@ struct PendGemv {
   unsigned lvl;
   std::vector<GemvDiags> dgs;  // launches of up to GemvDiags::MAX diagonals; empty: all-zero matrix
   const uint64_t *dspec = nullptr;  // x1's ModUp digits, precomputed (SpecModup), or null
+  // x = a - b is a queued he_sub (ew_lazy_sub): its polys a0 - b0, a1 - b1,
+  // formed where the inner products read them; null otherwise
+  const uint64_t *la0 = nullptr, *lb0 = nullptr, *la1 = nullptr, *lb1 = nullptr;
 };
 static std::vector<PendGemv> g_pgemv;
 
@@ -391,6 +394,22 @@ static void obj_free(void *vo)
       g_smu.valid = false;  // the speculative ModUp's public key
     if (g_spec_pk1_next >= lo && g_spec_pk1_next < hi)
       g_spec_pats_next.clear();
+    if (g_pew.count) {
+      // queued elementwise ops writing this block while no queued op reads it:
+      // their results can never be read, so they are dropped (HECTR's xdiff
+      // and udiff, src/hempc.c:269-270, once he_gemv read their operands)
+      auto in = [&](const uint64_t *p) { return p && p >= lo && p < hi; };
+      bool read = false;
+      for (unsigned j = 0; j < g_pew.count; j++)
+        read |= in(g_pew.op[j].a) || in(g_pew.op[j].b) || in(g_pew.op[j].s);
+      if (!read) {
+        unsigned w = 0;
+        for (unsigned j = 0; j < g_pew.count; j++)
+          if (!in(g_pew.op[j].out))
+            g_pew.op[w++] = g_pew.op[j];
+        g_pew.count = w;
+      }
+    }
     pool_free(o->data);
   }
   memset(o, 0, sizeof(*o));
@@ -1713,6 +1732,45 @@ static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
   return p;
 }
 
+// x = a - b, both polys written by queued he_sub ops that nothing else in the
+// queue touches (HECTR's xhat - xr and uhat - ur, src/hempc.c:253-256: the
+// queue then holds exactly those four ops)?  Then he_gemv leaves them queued
+// -- they run with the step's later elementwise ops -- and the inner products
+// form the difference where they read x (gemv_inner_kernel), which saves the
+// step a launch.  src: a0, b0, a1, b1.
+static bool ew_lazy_sub(const he_ct_t *x, const uint64_t *src[4])
+{
+  static const bool on = env_u("GPQHE_DEFER_SUB", 1);
+  if (!g_pew.count || !on)
+    return false;
+  const uint64_t *o0 = limb(x, 0, 0), *o1 = limb(x, 1, 0);
+  const EwOp *m0 = nullptr, *m1 = nullptr;
+  for (unsigned j = 0; j < g_pew.count; j++) {
+    const EwOp &o = g_pew.op[j];
+    if (o.kind != EW_SUB || o.lvl < x->nlimbs)
+      return false;
+    for (unsigned i = 0; i < g_pew.count; i++)  // no op reads what a queued op writes
+      if (g_pew.op[i].a == o.out || g_pew.op[i].b == o.out)
+        return false;
+    if (o.out == o0) {
+      if (m0)
+        return false;
+      m0 = &o;
+    } else if (o.out == o1) {
+      if (m1)
+        return false;
+      m1 = &o;
+    }
+  }
+  if (!m0 || !m1)
+    return false;
+  src[0] = m0->a;
+  src[1] = m0->b;
+  src[2] = m1->a;
+  src[3] = m1->b;
+  return true;
+}
+
 // Runs the queued gemvs: ModUp of every input in one pass (k_modup_ntt: one
 // fused launch at n <= 2^12), the inner products per gemv, and one ModDown
 // for each pair of outputs.  The arithmetic per
@@ -1751,10 +1809,20 @@ static void flush_gemvs()
     one &= q[i].dgs.size() == 1;
   if (one) {
     GemvJobs jobs;
-    for (unsigned i = 0; i < k; i++)
+    for (unsigned i = 0; i < k; i++) {
       jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, Dp[i], q[i].x0, q[i].x1, q[i].dgs[0], 0};
+      if (q[i].lb0) {  // the queued difference, formed in the kernel
+        jobs.j[i].x0 = q[i].la0;
+        jobs.j[i].x1 = q[i].la1;
+        jobs.j[i].y0 = q[i].lb0;
+        jobs.j[i].y1 = q[i].lb1;
+      }
+    }
     k_gemv_inner_jobs(jobs, k, lvl);
   } else {
+    for (unsigned i = 0; i < k; i++)
+      if (q[i].lb0)
+        flush_ew();  // the queued differences, materialised first
     for (unsigned i = 0; i < k; i++) {
       uint64_t *a = acc.p + (size_t)i * 2 * nm * n;
       bool started = false;
@@ -1827,7 +1895,12 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   HPROF("gemv");
   if (!G.init)
     gpqhe_die("context not initialised (hectx_init)");
-  flush_ew();  // x may be a queued difference
+  // x may be a queued difference: left queued when the inner products can
+  // form it (ew_lazy_sub, only with x's ModUp digits precomputed), else run
+  const uint64_t *lz[4];
+  const bool lazy = ew_lazy_sub(x, lz);
+  if (!lazy)
+    flush_ew();
   if (!g_pecd.empty() || !g_penc.empty())
     flush_pending();  // x may be a queued encryption
   const unsigned lvl = x->nlimbs, s = G.slots;
@@ -1843,6 +1916,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   if (may_clear) {
     // the diagonal cache may be cleared inside this call: unqueued form
     flush_gemvs();
+    flush_ew();
     gemv_now(y, Md, x, rk, lvl);
     return;
   }
@@ -1875,6 +1949,14 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
       g_spec_pk1_next = c.pk1;
       g_spec_pats_next.push_back({(unsigned)((c.sa - g_step_base) / 3), (unsigned)((c.sb - g_step_base) / 3)});
     }
+  }
+  if (lazy && pg.dspec) {
+    pg.la0 = lz[0];
+    pg.lb0 = lz[1];
+    pg.la1 = lz[2];
+    pg.lb1 = lz[3];
+  } else if (lazy) {
+    flush_ew();  // the ModUp reads x1 itself
   }
   const size_t mwords = 2 * (size_t)s * s;
   for (const GemvMat &gm : g_gemv_mats)

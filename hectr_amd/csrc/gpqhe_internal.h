@@ -372,6 +372,9 @@ struct GemvJob {
   const uint64_t *D, *x0, *x1;
   GemvDiags dg;
   int accumulate;
+  // non-null: the input is x - y, a queued he_sub not yet run (api.cpp
+  // he_gemv), formed where the kernel reads it
+  const uint64_t *y0 = nullptr, *y1 = nullptr;
 };
 struct GemvJobs {
   static constexpr unsigned MAX = 2;  // kernel arguments: ~0.8 KB per job

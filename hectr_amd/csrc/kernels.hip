@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 // (launch bound: two workgroups per CU, 128 VGPRs; the inverse takes 8-byte
 // twiddle entries (W8) to fit: with 16-byte ones it spilled 16 VGPRs, and at
 // one workgroup per CU it ran slower still)
-template <int LOGN2, bool INV, int QN, bool W8 = false>
+template <int LOGN2, bool INV, int QN, bool W8 = false, bool DIN = false>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                              const ModConst *mcs, unsigned members)
 {
@@ -396,9 +396,20 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
   uint64_t *lq = rt[qi];
   auto fetch = [&](uint64_t (&w)[8], unsigned p) {
     const uint64_t *x = s.limb(p * per + slot, logn) + toff;
+    if constexpr (INV && DIN) {
+      // the thread's round-C words 8 h + k of its row, 16-byte loads
+      const ulonglong2 *v2 = (const ulonglong2 *)(x + (row << LOGN2) + 8 * l);
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      w[k] = INV ? x[(th & ~63) * 8 + (th & 63) + 64 * k] : x[(row << LOGN2) + l + T::TA * k];
+      for (int i = 0; i < 4; i++) {
+        const ulonglong2 v = v2[i];
+        w[2 * i] = v.x;
+        w[2 * i + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        w[k] = INV ? x[(th & ~63) * 8 + (th & 63) + 64 * k] : x[(row << LOGN2) + l + T::TA * k];
+    }
   };
   with_arith(q, m, logn, tw, [&](const auto &ar0) {
     using A0 = std::decay_t<decltype(ar0)>;
@@ -429,7 +440,20 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
       if (p + QN < pb1)
         fetch(nx, p + QN);
       wave_sync();
-      rows8_tile_words<LOGN2, INV>(ar, w, o.limb(p * per + slot, logn) + toff, lq, n1 + row0, th);
+      if constexpr (INV && DIN) {
+        using V = typename std::decay_t<decltype(ar)>::V;
+        V r[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          r[k] = std::decay_t<decltype(ar)>::load(w[k]);
+        rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
+        uint64_t *y = o.limb(p * per + slot, logn) + toff;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+      } else {
+        rows8_tile_words<LOGN2, INV>(ar, w, o.limb(p * per + slot, logn) + toff, lq, n1 + row0, th);
+      }
     }
   });
 }
@@ -443,16 +467,32 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const double pass_bytes = 16.0 * n * s.count;
   // row pass: ntt_rows_q_kernel when every slot has polys enough to share
   // a workgroup's staged twiddles, else one tile per workgroup
+  auto cols_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
+    // (several tiles per workgroup with the next tile's words requested ahead
+    // measured slower: 86 -> 103 us forward, 73 -> 88 us inverse per 48-poly group)
+    if (inv)
+      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, in, out, logn, tw,
+                         G.dev.mc, post);
+    else
+      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, in, out, logn, tw,
+                         G.dev.mc, (const uint64_t *)nullptr);
+  };
   auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
     constexpr int QN = 2;
     const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
     if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
-      const unsigned members = std::max(1u, polys / (4 * QN));  // ~4 polys per quarter
+      // ~12 polys per quarter stream (two pair ranges per group of 48 polys:
+      // one wave of workgroups): forward 86.6 -> 76.2, inverse 99 -> 96 us per
+      // group against ~4 per quarter; ~24 (107 us inverse) and ~8 were slower,
+      // and a second poly in flight (PF = 2) no faster
+      const unsigned members = std::max(1u, polys / (12 * QN));
       // inverse: 8-byte staged twiddles (w only, quotient from the product):
       // 94 VGPRs, no spills (16-byte entries spilled 16 at this launch bound),
       // 107 -> 98 us per 48-poly group; the forward pass measured 86 -> 88 us
       // with them and keeps 16-byte (w, w/q) entries
-      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
+      // inverse: each thread loads its round-C words directly (16-byte loads,
+      // no transpose through LDS): 94.6 -> 88.4-90.5 us per 48-poly group
+      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
       hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
                          G.dev.mc, members);
     } else if (inv) {
@@ -466,8 +506,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   if (!inverse) {
     {
       ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
-      hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, s, o, logn, tw,
-                         G.dev.mc, (const uint64_t *)nullptr);
+      cols_launch(false, s, o);
     }
     ProfScope ps(KC_NTT3_ROWS_FWD, pass_bytes);
     rows_launch(false, o, o);
@@ -477,8 +516,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
       rows_launch(true, s, o);
     }
     ProfScope ps(KC_NTT2_COLS_INV, pass_bytes);
-    hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, o, o, logn, tw,
-                       G.dev.mc, post);
+    cols_launch(true, o, o);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -1899,7 +1937,7 @@ __global__ void __launch_bounds__(512) gemv_inner_kernel(GemvJobs jobs, unsigned
   // blockIdx.z: the job (gemvs queued together run in one launch)
   const GemvJob &job = jobs.j[blockIdx.z];
   uint64_t *acc = job.acc;
-  const uint64_t *D = job.D, *x0 = job.x0, *x1 = job.x1;
+  const uint64_t *D = job.D, *x0 = job.x0, *x1 = job.x1, *y0 = job.y0, *y1 = job.y1;
   const GemvDiags &dg = job.dg;
   const int accumulate = job.accumulate;
   const unsigned c = threadIdx.x % 64, gl = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
@@ -1922,9 +1960,12 @@ __global__ void __launch_bounds__(512) gemv_inner_kernel(GemvJobs jobs, unsigned
       }
     }
     if (t < lvl) {
-      s0 = add_mod(s0, mul_shoup(x0[tl + src], mm.pmod, mm.pmodp, mm.q), mm.q);
-      if (!evk)
-        s1 = add_mod(s1, mul_shoup(x1[tl + src], mm.pmod, mm.pmodp, mm.q), mm.q);
+      const uint64_t v0 = y0 ? sub_mod(x0[tl + src], y0[tl + src], mm.q) : x0[tl + src];
+      s0 = add_mod(s0, mul_shoup(v0, mm.pmod, mm.pmodp, mm.q), mm.q);
+      if (!evk) {
+        const uint64_t v1 = y1 ? sub_mod(x1[tl + src], y1[tl + src], mm.q) : x1[tl + src];
+        s1 = add_mod(s1, mul_shoup(v1, mm.pmod, mm.pmodp, mm.q), mm.q);
+      }
     }
     const uint64_t w = dg.pt[e][tl + k];
     a0 = add_mod(a0, mul_mod(w, s0, mm), mm.q);
