@@ -600,6 +600,56 @@ def test_speculative_encryption_noise(oracle, product):
         assert np.array_equal(x, y), f"object {i} differs"
 
 
+def test_gemv_of_queued_differences(oracle, product):
+    """HECTR's regulator step (src/hempc.c:253-270) repeated: he_sub x2 of
+    fresh encryptions, he_gemv of each difference (api.cpp ew_lazy_sub: from
+    the second step on, the subs stay queued and gemv_inner_kernel forms the
+    differences from their operands), then he_add / he_neg and the decode.
+    Variants per step: the differences freed unread (their queued subs are
+    dropped), read back after the gemvs (the subs must still run), an operand
+    of a sub overwritten after the gemvs (the gemv must see the old value),
+    and GPQHE-style non-speculated steps (a different number of encryptions)
+    -- every exported object and decoded value bit-exact vs the oracle."""
+    init_both(oracle, product, "ref")
+    rng = np.random.default_rng(31)
+    s = oracle.slots
+    M1 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
+    M2 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
+    plan = ["free", "free", "read", "free", "clobber", "free", "four", "free", "free"]
+    zs = [[rng.uniform(-1, 1, s) + 0j for _ in range(5)] for _ in plan]
+    out = {}
+    for e in (oracle, product):
+        pk, sk, rk, _ = keys(e, rot=True)
+        res = []
+        for kind, zz in zip(plan, zs):
+            cnt = 4 if kind == "four" else 5
+            cts = [e.encrypt(z, pk) for z in zz[:cnt]]
+            xd, ud = e.ct(), e.ct()
+            e.sub(xd, cts[0], cts[1])
+            e.sub(ud, cts[2], cts[3])
+            ya, yb = e.ct(), e.ct()
+            e.gemv(ya, M1.ravel(), xd, rk)
+            e.gemv(yb, M2.ravel(), ud, rk)
+            du = e.ct()
+            e.add(du, ya, yb)
+            e.neg(du)
+            if kind == "read":
+                res += [e.export(xd), e.export(ud)]
+            if kind == "clobber":
+                e.add(cts[0], cts[0], cts[1])  # an operand of the first sub
+                res.append(e.export(cts[0]))
+            res += [e.export(ya), e.export(yb), e.export(du)]
+            for x in (xd, ud, ya, yb):
+                e.free(x)
+            res.append(e.decrypt(du, sk))
+            for x in cts + [du]:
+                e.free(x)
+        out[e.name] = res
+    assert len(out["oracle"]) == len(out["product"])
+    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
+        assert np.array_equal(x, y), f"object {i} differs"
+
+
 @pytest.mark.parametrize("name", ["ref", "c1"])
 def test_plaintext_ops_rot0_and_queue_overflow(oracle, product, name):
     """he_add_pt (out != a: a queued copy the add then reads; and in place),
