@@ -274,6 +274,8 @@ static EwProg g_pew{};
 
 static void flush_pending();
 static void flush_gemvs();
+static unsigned env_u(const char *name, unsigned dflt);
+static bool g_spec_early = false;  // the next step's speculation rides on this step's gemv / ModDown (spec_attach)
 
 static void flush_ew()
 {
@@ -380,12 +382,34 @@ static bool drop_dead_encode(const uint64_t *data)
   return true;
 }
 
+// Every queued encode dropped (its plaintext freed) and the queued
+// encryptions are exactly the speculated ones (SpecNoise): they run now --
+// only the combine, from the speculative noise and the plaintexts'
+// coefficients -- so it overlaps the caller's host work up to its next call
+// that needs them (HECTR's horizon matrices in ctr_hempc, src/hempc.c:225-240)
+// instead of starting at that call.  GPQHE_SPEC_EARLY=0: at that call.
+static void spec_flush_early()
+{
+  static const bool on = env_u("GPQHE_SPEC_EARLY", 1) != 0;
+  if (!on || !g_spec.valid || g_penc.empty() || g_penc.size() != g_spec.k || !g_pgemv.empty() || g_pew.count ||
+      g_penc[0].stream != g_spec.base || g_penc[0].lvl != g_spec.lvl)
+    return;
+  for (const PendEcd &e : g_pecd)
+    if (e.dst)
+      return;
+  flush_pending();
+}
+
 static void obj_free(void *vo)
 {
   // a queued encode / encryption / gemv may still use the payload (queued
   // elementwise ops keep their order with any later user of the block)
-  if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty()) && !drop_dead_encode(OB(vo)->data))
-    check_ctx();
+  bool dropped = false;
+  if (G.init && (!g_pgemv.empty() || !g_pecd.empty() || !g_penc.empty())) {
+    dropped = drop_dead_encode(OB(vo)->data);
+    if (!dropped)
+      check_ctx();
+  }
   he_ct_t *o = OB(vo);
   if (o->data && G.init) {
     prov_forget(o->data, (size_t)o->cap << G.logn);
@@ -413,6 +437,8 @@ static void obj_free(void *vo)
     pool_free(o->data);
   }
   memset(o, 0, sizeof(*o));
+  if (dropped)
+    spec_flush_early();
 }
 
 static uint64_t next_stream()
@@ -1229,6 +1255,73 @@ static bool spec_launch()
   return true;
 }
 
+// flush_gemvs of a small-N step: the next step's speculation (the same noise
+// and ModUp spec_launch runs after the decode) is carried by this step's
+// gemv_inner and ModDown launches as extra workgroups (SpecAttach), where it
+// uses the CUs those few-workgroup kernels leave idle.  Only when the three
+// launches take it: the gemvs in one inner-product launch (one), the noise
+// sampling fits its z slice, and the ModDown of P q_top drops K + 1 >= 2
+// limbs (the two-launch form).  The buffers are free: this step's combine and
+// inner products, which read the current speculation, run before in stream
+// order.  (A second stream for this work measured 3x slower)
+static bool spec_attach(bool one, unsigned glvl)
+{
+  static const bool on = env_u("GPQHE_SPEC", 1) != 0 && env_u("GPQHE_SPEC_ATTACH", 1) != 0;
+  const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
+  if (!on || !one || !k || !lvl || k > GPQHE_MAXGRP || !defer_ok(0) || G.logn < 10 || G.logn > 12 || G.K < 1)
+    return false;
+  if ((size_t)3 * k * (G.n / 512) > (size_t)(G.n / 64) * (glvl + G.K))
+    return false;
+  const size_t w = (size_t)lvl << G.logn, words = 3 * (size_t)k * w;
+  if (g_spec.words != words) {
+    pool_free(g_spec.buf);  // stream-ordered: its last reader was launched before
+    g_spec.buf = (uint64_t *)pool_alloc(words * 8);
+    g_spec.words = words;
+  }
+  unsigned mods[GPQHE_MAXMOD];
+  for (unsigned l = 0; l < lvl; l++)
+    mods[l] = l;
+  g_sa = SpecAttach{};
+  g_sa.noise = limbset(g_spec.buf, mods, lvl, 3 * k, w);
+  g_sa.stream = G.counter;
+  g_sa.npoly = 3 * k;
+  g_sa.sample = g_sa.ntt = true;
+  g_spec.base = G.counter;
+  g_spec.k = k;
+  g_spec.lvl = lvl;
+  g_spec.valid = true;
+  g_smu.valid = false;
+  const std::vector<SpecPat> &pats = g_spec_pats_next;
+  bool ok = !pats.empty() && g_spec_pk1_next && lvl >= 2;
+  for (const SpecPat &p : pats)
+    ok &= p.oa < k && p.ob < k;
+  if (ok) {
+    const unsigned np = (unsigned)pats.size(), nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+    const size_t dw = (size_t)np * ndig * nm << G.logn;
+    if (g_smu.dwords != dw) {
+      pool_free(g_smu.D);
+      g_smu.D = (uint64_t *)pool_alloc(dw * 8);
+      g_smu.dwords = dw;
+    }
+    for (unsigned i = 0; i < np; i++) {
+      g_sa.cd.va[i] = g_spec.buf + (size_t)3 * pats[i].oa * w;
+      g_sa.cd.vb[i] = g_spec.buf + (size_t)3 * pats[i].ob * w;
+    }
+    g_sa.D = g_smu.D;
+    g_sa.d_stride = (size_t)ndig * nm << G.logn;
+    g_sa.np = np;
+    g_sa.pk1 = g_spec_pk1_next;
+    g_sa.lvl = lvl;
+    g_sa.modup = true;
+    g_smu.pats = pats;
+    g_smu.base = g_spec.base;
+    g_smu.pk1 = g_spec_pk1_next;
+    g_smu.lvl = lvl;
+    g_smu.valid = true;
+  }
+  return true;
+}
+
 extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
 {
   HPROF("dcd");
@@ -1250,7 +1343,9 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     const EwProg p = g_pew;
     g_pew.count = 0;
     k_ew_decode(p, zd, pt->data, pt->nlimbs, slots, pt->scale, c.p);
-    if (spec_launch()) {
+    const bool early = g_spec_early;
+    g_spec_early = false;
+    if (!early && spec_launch()) {
       HIP_CHECK(hipEventSynchronize(g_dcd_ev));  // the decode, not the noise behind it
     } else {
       HIP_CHECK(hipStreamSynchronize(G.stream));
@@ -1808,6 +1903,8 @@ static void flush_gemvs()
   for (unsigned i = 0; i < k; i++)
     one &= q[i].dgs.size() == 1;
   if (one) {
+    if (!g_spec_early && spec_attach(true, lvl))
+      g_spec_early = true;
     GemvJobs jobs;
     for (unsigned i = 0; i < k; i++) {
       jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, Dp[i], q[i].x0, q[i].x1, q[i].dgs[0], 0};
@@ -1838,6 +1935,8 @@ static void flush_gemvs()
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 2, lvl, 1);
   else
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 4, lvl, 1, q[1].y);
+  if (g_sa.sample || g_sa.ntt || g_sa.modup)
+    gpqhe_die("flush_gemvs: attached speculative work not taken (%d %d %d)", g_sa.sample, g_sa.ntt, g_sa.modup);
 }
 
 // Unqueued he_gemv for matrices whose diagonals may overflow the cache: a

@@ -603,6 +603,22 @@ __global__ void __launch_bounds__(512) ntt_small_kernel(LimbSet s, Tw2 tw, const
   });
 }
 
+// In-place forward transform of limb v of s (ntt_small_kernel<LOGN, false>
+// without a lift), for workgroups attached to another launch (SpecAttach).
+template <int LOGN>
+__device__ __forceinline__ void ntt_fwd_small_body(const LimbSet &s, const Tw2 &tw, const ModConst *mcs, unsigned v,
+                                                   uint64_t *lds)
+{
+  uint64_t *x = s.limb(v, LOGN);
+  const unsigned m = s.mod(v);
+  const ModConst mc = mcs[m];
+  with_arith(mc.q, m, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds, [&](int, int i) { return A::load(x[i]); }, [&](int, int i, typename A::V a) { x[i] = ar.canon(a); });
+  });
+}
+
 // The same lift + forward transform with the (few) coefficients passed by
 // value in the kernel arguments: group g's value j at ca.v[g row + j] is
 // coefficient j 2^clog, the others are 0.  No upload, no host-memory reads.
@@ -999,6 +1015,28 @@ __global__ void sample_small_kernel(LimbSet dst, unsigned logn, ChachaKey key, u
 // k_sample_small calls in that order.  With ec, encryption e's e0 (y = 3 e + 1)
 // also takes the integer coefficients of its plaintext (EncCoef): the caller
 // then combines without m, as NTT(e0 + m) = NTT(e0) + NTT(m) mod q.
+__device__ __forceinline__ int enc_noise_value(const ChachaKey &key, uint64_t stream, unsigned y, unsigned k)
+{
+  uint32_t b[16];
+  chacha20_block(b, key, stream + y, k);
+  if (y % 3)  // (v, e0, e1) per encryption: ternary v, CBD e0 / e1
+    return __popc(b[0] & 0x1FFFFFu) - __popc(b[1] & 0x1FFFFFu);
+  const uint32_t r = b[0] & 3u;
+  return r < 2 ? 0 : (r == 2 ? 1 : -1);
+}
+
+// Coefficient k of noise poly y into its limbs (sample_enc_kernel without a
+// plaintext; the attached sampler of gemv_inner_kernel).
+__device__ __forceinline__ void enc_noise_store(const LimbSet &dst, unsigned logn, const ChachaKey &key,
+                                                uint64_t stream, const ModConst *mc, unsigned y, unsigned k)
+{
+  const int v = enc_noise_value(key, stream, y, k);
+  for (unsigned l = y * dst.per; l < (y + 1) * dst.per; l++) {
+    const uint64_t q = mc[dst.mod(l)].q;
+    dst.limb(l, logn)[k] = v >= 0 ? (uint64_t)v : q - (uint64_t)(-v);
+  }
+}
+
 __global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, const ModConst *mc,
                                   EncCoef ec, int has_ec)
 {
@@ -1006,15 +1044,7 @@ __global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uin
   if (k >= (1u << logn))
     return;
   const unsigned y = blockIdx.y;
-  uint32_t b[16];
-  chacha20_block(b, key, stream + y, k);
-  int v;
-  if (y % 3) {  // (v, e0, e1) per encryption: ternary v, CBD e0 / e1
-    v = __popc(b[0] & 0x1FFFFFu) - __popc(b[1] & 0x1FFFFFu);
-  } else {
-    const uint32_t r = b[0] & 3u;
-    v = r < 2 ? 0 : (r == 2 ? 1 : -1);
-  }
+  const int v = enc_noise_value(key, stream, y, k);
   bool addm = false;
   int64_t mco = 0;
   if (has_ec && y % 3 == 1) {
@@ -1929,10 +1959,25 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
 // Galois element come from the kernel arguments by scalar loads: per-lane reads
 // of by-value arguments took ~3.5 us more per launch (scripts/ubench_small).
 // grid: (n / 64, nm, jobs), 512 threads.
+// sp.npoly > 0: the last z slice samples the next step's noise instead
+// (SpecAttach): workgroup (x, y) of it covers coefficients [512 b, 512 b + 512)
+// of noise poly b / (n / 512), b = y gridDim.x + x.
+struct SpecSmp {
+  LimbSet dst;
+  ChachaKey key;
+  uint64_t stream;
+  unsigned npoly;
+};
 __global__ void __launch_bounds__(512) gemv_inner_kernel(GemvJobs jobs, unsigned logn, unsigned lvl, unsigned L,
                                                           unsigned nm, unsigned nmod, unsigned ndig,
-                                                          const ModConst *mc)
+                                                          const ModConst *mc, SpecSmp sp)
 {
+  if (sp.npoly && blockIdx.z == gridDim.z - 1) {
+    const unsigned b = blockIdx.y * gridDim.x + blockIdx.x, bpp = (1u << logn) / 512;
+    if (b < sp.npoly * bpp)
+      enc_noise_store(sp.dst, logn, sp.key, sp.stream, mc, b / bpp, (b % bpp) * 512 + threadIdx.x);
+    return;
+  }
   __shared__ uint64_t part[2][8][64];
   // blockIdx.z: the job (gemvs queued together run in one launch)
   const GemvJob &job = jobs.j[blockIdx.z];
@@ -1993,8 +2038,17 @@ void k_gemv_inner_jobs(const GemvJobs &jobs, unsigned njobs, unsigned lvl)
   for (unsigned i = 0; i < njobs; i++)
     diags += jobs.j[i].dg.count;
   ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * diags * (ndig * nm + 2 * nm + 2 * lvl));
-  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 64, nm, njobs), dim3(512), 0, G.stream, jobs, G.logn, lvl, G.L,
-                     nm, G.nmod, ndig, G.dev.mc);
+  // the next step's noise sampling rides along in one more z slice (g_sa)
+  SpecSmp sp{};
+  if (g_sa.sample && G.n >= 512 && (size_t)g_sa.npoly * (G.n / 512) <= (size_t)(G.n / 64) * nm) {
+    sp.dst = g_sa.noise;
+    sp.key = G.key;
+    sp.stream = g_sa.stream;
+    sp.npoly = g_sa.npoly;
+    g_sa.sample = false;
+  }
+  hipLaunchKernelGGL(gemv_inner_kernel, dim3(G.n / 64, nm, njobs + (sp.npoly ? 1 : 0)), dim3(512), 0, G.stream, jobs,
+                     G.logn, lvl, G.L, nm, G.nmod, ndig, G.dev.mc, sp);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -2866,13 +2920,12 @@ __global__ void down_combine_kernel(uint64_t *out, uint64_t *out2, unsigned half
 // e1_b) as enc_batch_kernel and the queued he_sub form it (the speculative
 // ModUp of the small-N step, api.cpp SpecModup).
 template <int LOGN, bool DIFF>
-__global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1, size_t d_stride, unsigned lvl,
-                                                           unsigned L, unsigned nm, Tw2 tw, UpTable tab,
-                                                           const ModConst *mcs, C1Diffs cd, const uint64_t *pk1)
+__device__ __forceinline__ void modup_small_body(uint64_t *D, const XPtrs &x1, size_t d_stride, unsigned lvl,
+                                                 unsigned L, unsigned nm, const Tw2 &tw, const UpTable &tab,
+                                                 const ModConst *mcs, const C1Diffs &cd, const uint64_t *pk1,
+                                                 unsigned t, unsigned j, unsigned p, uint64_t *lds)
 {
   constexpr int n = 1 << LOGN;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
-  const unsigned t = blockIdx.x, j = blockIdx.y, p = blockIdx.z;
   const UpDigit *dg = tab.dig + j;
   const unsigned lo = dg->lo, na = dg->na;
   const uint64_t *x = x1.p[p];
@@ -2933,6 +2986,29 @@ __global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1,
         [&](int, int e, typename A::V a) { out[e] = ar.canon(a); });
   });
 }
+
+template <int LOGN, bool DIFF>
+__global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1, size_t d_stride, unsigned lvl,
+                                                           unsigned L, unsigned nm, Tw2 tw, UpTable tab,
+                                                           const ModConst *mcs, C1Diffs cd, const uint64_t *pk1)
+{
+  __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN];
+  modup_small_body<LOGN, DIFF>(D, x1, d_stride, lvl, L, nm, tw, tab, mcs, cd, pk1, blockIdx.x, blockIdx.y, blockIdx.z,
+                               lds);
+}
+
+SpecAttach g_sa;
+struct SpecNtt {  // down_inv_small_kernel's attached forward transforms
+  LimbSet s;
+};
+struct SpecUp {  // down_fwd_small_kernel's attached ModUp of c1 differences
+  UpTable tab;
+  uint64_t *D;
+  size_t d_stride;
+  C1Diffs cd;
+  const uint64_t *pk1;
+  unsigned lvl;
+};
 
 // Fused small-N ModDown (+ rescale by its mode): output slot t of poly p in
 // one workgroup: the inverse transform of each dropped limb, the conversion
@@ -2997,13 +3073,20 @@ __global__ void __launch_bounds__(512) moddown_small_kernel(uint64_t *out, uint6
 // one workgroup (the fused kernel's chain is nd + 1 transforms, this one's 2).
 // down_inv_small_kernel, grid (nd, npoly): Y[p][d] = INTT(X[p][keep + d])
 // [(D/d)^-1]_d, coefficient domain, canonical (the fused kernel's y).
+// (1-D grid: nd npoly workgroups, then sn.count more that run the forward
+// transform of limb b - nd npoly of sn.s in place: the next step's noise,
+// SpecAttach)
 template <int LOGN>
 __global__ void __launch_bounds__(512) down_inv_small_kernel(uint64_t *Y, const uint64_t *X, size_t x_pstride,
                                                               unsigned lvl, unsigned L, Tw2 tw, DownTable tab,
-                                                              const ModConst *mcs)
+                                                              const ModConst *mcs, unsigned npoly, SpecNtt sn)
 {
   __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN];
-  const unsigned d = blockIdx.x, p = blockIdx.y;
+  if (blockIdx.x >= tab.nd * npoly) {
+    ntt_fwd_small_body<LOGN>(sn.s, tw, mcs, blockIdx.x - tab.nd * npoly, lds);
+    return;
+  }
+  const unsigned d = blockIdx.x % tab.nd, p = blockIdx.x / tab.nd;
   const unsigned bd = tab.keep + d, md = basis_mod(bd, lvl, L);
   const ModConst mc = mcs[md];
   const uint64_t *src = X + p * x_pstride + ((size_t)bd << LOGN);
@@ -3020,15 +3103,25 @@ __global__ void __launch_bounds__(512) down_inv_small_kernel(uint64_t *Y, const 
 // down_fwd_small_kernel, grid (keep, npoly): conversion sum of Y to slot t,
 // forward transform mod q_t, out = (X[t] - conv) [D^-1]_t, as the fused
 // kernel (thread th holds elements th + k n/8 before a forward transform).
+// (1-D grid: keep npoly workgroups, then su.np nm ndig more that run the
+// speculative ModUp of the next step's gemv inputs, modup_small_body<DIFF>:
+// SpecAttach)
 template <int LOGN>
 __global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint64_t *out2, unsigned half,
                                                               size_t out_pstride, const uint64_t *Y,
                                                               const uint64_t *X, size_t x_pstride, unsigned lvl,
-                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs)
+                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs,
+                                                              unsigned npoly, SpecUp su)
 {
   constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
-  const unsigned t = blockIdx.x, p = blockIdx.y;
+  if (blockIdx.x >= tab.keep * npoly) {
+    const unsigned b = blockIdx.x - tab.keep * npoly;
+    modup_small_body<LOGN, true>(su.D, XPtrs{}, su.d_stride, su.lvl, L, su.tab.nm, tw, su.tab, mcs, su.cd, su.pk1,
+                                 b % su.tab.nm, (b / su.tab.nm) % su.tab.ndig, b / (su.tab.nm * su.tab.ndig), lds);
+    return;
+  }
+  const unsigned t = blockIdx.x % tab.keep, p = blockIdx.x / tab.keep;
   const int th = threadIdx.x;
   // X's words of this thread's outputs (the forward transform's last round
   // leaves elements 8 th + k with the thread), requested before the
@@ -3156,11 +3249,30 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
     const unsigned half = out2 ? npoly / 2 : npoly;
     if (tab.nd >= 2) {
       uint64_t *Y = (uint64_t *)pool_alloc(((size_t)npoly * tab.nd << G.logn) * 8);
+      // the next step's speculative transforms and ModUp ride along (g_sa)
+      SpecNtt sn{};
+      SpecUp su{};
+      unsigned xn = 0, xu = 0;
+      if (g_sa.ntt) {
+        sn.s = g_sa.noise;
+        xn = g_sa.noise.count;
+        g_sa.ntt = false;
+      }
+      if (g_sa.modup) {
+        su.tab = up_table(g_sa.lvl);
+        su.D = g_sa.D;
+        su.d_stride = g_sa.d_stride;
+        su.cd = g_sa.cd;
+        su.pk1 = g_sa.pk1;
+        su.lvl = g_sa.lvl;
+        xu = g_sa.np * su.tab.nm * su.tab.ndig;
+        g_sa.modup = false;
+      }
       auto go2 = [&](auto kinv, auto kfwd) {
-        hipLaunchKernelGGL(kinv, dim3(tab.nd, npoly), dim3(G.n / 8), 0, G.stream, Y, X, x_pstride, lvl, G.L, tw, tab,
-                           G.dev.mc);
-        hipLaunchKernelGGL(kfwd, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, Y,
-                           X, x_pstride, lvl, G.L, tw, tab, G.dev.mc);
+        hipLaunchKernelGGL(kinv, dim3(tab.nd * npoly + xn), dim3(G.n / 8), 0, G.stream, Y, X, x_pstride, lvl, G.L, tw,
+                           tab, G.dev.mc, npoly, sn);
+        hipLaunchKernelGGL(kfwd, dim3(tab.keep * npoly + xu), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride,
+                           Y, X, x_pstride, lvl, G.L, tw, tab, G.dev.mc, npoly, su);
       };
       if (G.logn == 12)
         go2(down_inv_small_kernel<12>, down_fwd_small_kernel<12>);
