@@ -235,6 +235,15 @@ struct SpecModup {
   bool valid = false;
 };
 static SpecModup g_smu;
+// spec_attach's ModUp, launched behind the decode (spec_modup_launch)
+struct SpecModupNext {
+  C1Diffs cd{};
+  unsigned np = 0, lvl = 0;
+  size_t d_stride = 0;
+  const uint64_t *pk1 = nullptr;
+  bool pending = false;
+};
+static SpecModupNext g_smu_next;
 
 static void prov_forget(const void *obj_data, size_t pstride_words)
 {
@@ -293,6 +302,7 @@ static void check_ctx()
   // a non-queued entry point: it may write any object (C1Prov)
   g_prov.clear();
   g_smu.valid = false;
+  g_smu_next.pending = false;
   flush_ew();
   if (!g_pgemv.empty())
     flush_gemvs();
@@ -416,6 +426,8 @@ static void obj_free(void *vo)
     const uint64_t *lo = o->data, *hi = o->data + ((size_t)o->npoly * o->cap << G.logn);
     if (g_smu.pk1 >= lo && g_smu.pk1 < hi)
       g_smu.valid = false;  // the speculative ModUp's public key
+    if (g_smu_next.pk1 >= lo && g_smu_next.pk1 < hi)
+      g_smu_next.pending = false;  // (its pending launch reads it)
     if (g_spec_pk1_next >= lo && g_spec_pk1_next < hi)
       g_spec_pats_next.clear();
     if (g_pew.count) {
@@ -524,6 +536,7 @@ static void set_seed_words(uint64_t seed)
   G.counter = 0;
   g_spec.valid = false;  // noise of the old key
   g_smu.valid = false;
+  g_smu_next.pending = false;
 }
 
 extern "C" void gpqhe_set_seed(uint64_t seed)
@@ -719,6 +732,8 @@ extern "C" void hectx_exit(void)
   g_spec = SpecNoise{};  // its blocks go with the pool
   g_spec_next_k = 0;
   g_smu = SpecModup{};
+  g_smu_next = SpecModupNext{};
+  g_sa = SpecAttach{};
   g_prov.clear();
   g_spec_pats_next.clear();
   g_spec_pk1_next = nullptr;
@@ -1204,6 +1219,7 @@ static bool spec_launch()
 {
   static const bool on = env_u("GPQHE_SPEC", 1) != 0;
   const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
+  g_smu_next.pending = false;  // superseded
   if (!on || !k || !lvl || k > GPQHE_MAXGRP || !defer_ok(0))
     return false;
   if (!g_dcd_ev)
@@ -1282,6 +1298,7 @@ static bool spec_attach(bool one, unsigned glvl)
   for (unsigned l = 0; l < lvl; l++)
     mods[l] = l;
   g_sa = SpecAttach{};
+  g_smu_next.pending = false;
   g_sa.noise = limbset(g_spec.buf, mods, lvl, 3 * k, w);
   g_sa.stream = G.counter;
   g_sa.npoly = 3 * k;
@@ -1303,22 +1320,34 @@ static bool spec_attach(bool one, unsigned glvl)
       g_smu.D = (uint64_t *)pool_alloc(dw * 8);
       g_smu.dwords = dw;
     }
+    // the ModUp itself runs behind this step's decode (he_dcd_ex), in the
+    // device time the caller's host work leaves idle: attached to the
+    // ModDown it lengthened the chain the decode waits on (13.9 -> 21.5 us)
     for (unsigned i = 0; i < np; i++) {
-      g_sa.cd.va[i] = g_spec.buf + (size_t)3 * pats[i].oa * w;
-      g_sa.cd.vb[i] = g_spec.buf + (size_t)3 * pats[i].ob * w;
+      g_smu_next.cd.va[i] = g_spec.buf + (size_t)3 * pats[i].oa * w;
+      g_smu_next.cd.vb[i] = g_spec.buf + (size_t)3 * pats[i].ob * w;
     }
-    g_sa.D = g_smu.D;
-    g_sa.d_stride = (size_t)ndig * nm << G.logn;
-    g_sa.np = np;
-    g_sa.pk1 = g_spec_pk1_next;
-    g_sa.lvl = lvl;
-    g_sa.modup = true;
+    g_smu_next.np = np;
+    g_smu_next.d_stride = (size_t)ndig * nm << G.logn;
+    g_smu_next.pk1 = g_spec_pk1_next;
+    g_smu_next.lvl = lvl;
+    g_smu_next.pending = true;
     g_smu.pats = pats;
     g_smu.base = g_spec.base;
     g_smu.pk1 = g_spec_pk1_next;
     g_smu.lvl = lvl;
-    g_smu.valid = true;
   }
+  return true;
+}
+
+// The ModUp spec_attach left pending, behind the decode: true if launched.
+static bool spec_modup_launch()
+{
+  if (!g_smu_next.pending)
+    return false;
+  g_smu_next.pending = false;
+  k_modup_ntt_diffs(g_smu.D, g_smu_next.cd, g_smu_next.np, g_smu_next.d_stride, g_smu_next.pk1, g_smu_next.lvl);
+  g_smu.valid = true;
   return true;
 }
 
@@ -1345,7 +1374,16 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     k_ew_decode(p, zd, pt->data, pt->nlimbs, slots, pt->scale, c.p);
     const bool early = g_spec_early;
     g_spec_early = false;
-    if (!early && spec_launch()) {
+    bool spec = false;
+    if (early && g_smu_next.pending) {
+      if (!g_dcd_ev)
+        HIP_CHECK(hipEventCreateWithFlags(&g_dcd_ev, hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(g_dcd_ev, G.stream));
+      spec = spec_modup_launch();
+    } else if (!early) {
+      spec = spec_launch();
+    }
+    if (spec) {
       HIP_CHECK(hipEventSynchronize(g_dcd_ev));  // the decode, not the noise behind it
     } else {
       HIP_CHECK(hipStreamSynchronize(G.stream));
@@ -1935,8 +1973,8 @@ static void flush_gemvs()
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 2, lvl, 1);
   else
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 4, lvl, 1, q[1].y);
-  if (g_sa.sample || g_sa.ntt || g_sa.modup)
-    gpqhe_die("flush_gemvs: attached speculative work not taken (%d %d %d)", g_sa.sample, g_sa.ntt, g_sa.modup);
+  if (g_sa.sample || g_sa.ntt)
+    gpqhe_die("flush_gemvs: attached speculative work not taken (%d %d)", g_sa.sample, g_sa.ntt);
 }
 
 // Unqueued he_gemv for matrices whose diagonals may overflow the cache: a

@@ -355,22 +355,16 @@ struct XPtrs {
   static constexpr unsigned MAX = 8;
   const uint64_t *p[MAX];
 };
-// The next small-N step's speculative work carried by this step's kernels
-// (api.cpp flush_gemvs; no launches of its own): extra workgroups of
-// gemv_inner_kernel sample the noise (sample), of down_inv_small_kernel run its
-// forward transforms (ntt), of down_fwd_small_kernel form the gemv inputs' c1
-// differences and their ModUp (modup).  Each launcher takes its part and
-// clears the flag; the values equal those of the separate launches.
+// The next small-N step's noise carried by this step's kernels (api.cpp
+// flush_gemvs; no launches of its own): extra workgroups of
+// gemv_inner_kernel sample it (sample), of down_inv_small_kernel run its
+// forward transforms (ntt).  Each launcher takes its part and clears the
+// flag; the values equal those of the separate launches.
 struct SpecAttach {
-  bool sample = false, ntt = false, modup = false;
+  bool sample = false, ntt = false;
   LimbSet noise{};      // 3k polys x lvl limbs (per = lvl)
   uint64_t stream = 0;  // poly y draws from ChaCha stream stream + y
   unsigned npoly = 0;   // 3k
-  uint64_t *D = nullptr;
-  size_t d_stride = 0;
-  C1Diffs cd{};
-  unsigned np = 0, lvl = 0;
-  const uint64_t *pk1 = nullptr;
 };
 extern SpecAttach g_sa;
 void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, unsigned lvl);

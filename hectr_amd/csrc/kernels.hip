@@ -3001,14 +3001,6 @@ SpecAttach g_sa;
 struct SpecNtt {  // down_inv_small_kernel's attached forward transforms
   LimbSet s;
 };
-struct SpecUp {  // down_fwd_small_kernel's attached ModUp of c1 differences
-  UpTable tab;
-  uint64_t *D;
-  size_t d_stride;
-  C1Diffs cd;
-  const uint64_t *pk1;
-  unsigned lvl;
-};
 
 // Fused small-N ModDown (+ rescale by its mode): output slot t of poly p in
 // one workgroup: the inverse transform of each dropped limb, the conversion
@@ -3103,25 +3095,15 @@ __global__ void __launch_bounds__(512) down_inv_small_kernel(uint64_t *Y, const 
 // down_fwd_small_kernel, grid (keep, npoly): conversion sum of Y to slot t,
 // forward transform mod q_t, out = (X[t] - conv) [D^-1]_t, as the fused
 // kernel (thread th holds elements th + k n/8 before a forward transform).
-// (1-D grid: keep npoly workgroups, then su.np nm ndig more that run the
-// speculative ModUp of the next step's gemv inputs, modup_small_body<DIFF>:
-// SpecAttach)
 template <int LOGN>
 __global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint64_t *out2, unsigned half,
                                                               size_t out_pstride, const uint64_t *Y,
                                                               const uint64_t *X, size_t x_pstride, unsigned lvl,
-                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs,
-                                                              unsigned npoly, SpecUp su)
+                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs)
 {
   constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
-  if (blockIdx.x >= tab.keep * npoly) {
-    const unsigned b = blockIdx.x - tab.keep * npoly;
-    modup_small_body<LOGN, true>(su.D, XPtrs{}, su.d_stride, su.lvl, L, su.tab.nm, tw, su.tab, mcs, su.cd, su.pk1,
-                                 b % su.tab.nm, (b / su.tab.nm) % su.tab.ndig, b / (su.tab.nm * su.tab.ndig), lds);
-    return;
-  }
-  const unsigned t = blockIdx.x % tab.keep, p = blockIdx.x / tab.keep;
+  const unsigned t = blockIdx.x, p = blockIdx.y;
   const int th = threadIdx.x;
   // X's words of this thread's outputs (the forward transform's last round
   // leaves elements 8 th + k with the thread), requested before the
@@ -3251,28 +3233,17 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
       uint64_t *Y = (uint64_t *)pool_alloc(((size_t)npoly * tab.nd << G.logn) * 8);
       // the next step's speculative transforms and ModUp ride along (g_sa)
       SpecNtt sn{};
-      SpecUp su{};
-      unsigned xn = 0, xu = 0;
+      unsigned xn = 0;
       if (g_sa.ntt) {
         sn.s = g_sa.noise;
         xn = g_sa.noise.count;
         g_sa.ntt = false;
       }
-      if (g_sa.modup) {
-        su.tab = up_table(g_sa.lvl);
-        su.D = g_sa.D;
-        su.d_stride = g_sa.d_stride;
-        su.cd = g_sa.cd;
-        su.pk1 = g_sa.pk1;
-        su.lvl = g_sa.lvl;
-        xu = g_sa.np * su.tab.nm * su.tab.ndig;
-        g_sa.modup = false;
-      }
       auto go2 = [&](auto kinv, auto kfwd) {
         hipLaunchKernelGGL(kinv, dim3(tab.nd * npoly + xn), dim3(G.n / 8), 0, G.stream, Y, X, x_pstride, lvl, G.L, tw,
                            tab, G.dev.mc, npoly, sn);
-        hipLaunchKernelGGL(kfwd, dim3(tab.keep * npoly + xu), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride,
-                           Y, X, x_pstride, lvl, G.L, tw, tab, G.dev.mc, npoly, su);
+        hipLaunchKernelGGL(kfwd, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, Y, X,
+                           x_pstride, lvl, G.L, tw, tab, G.dev.mc);
       };
       if (G.logn == 12)
         go2(down_inv_small_kernel<12>, down_fwd_small_kernel<12>);
