@@ -318,6 +318,42 @@ def test_batch_real_encryptions_decode(product, name):
         product.free(ct)
 
 
+@pytest.mark.parametrize("frac,ok", [(0.8, True), (1.3, False)])
+def test_batch_level0_headroom(product, frac, ok):
+    """The bench's < 2^51 set (q0 51 bits at Delta = 2^50) keeps about one bit
+    of integer headroom once a product lands on q0 alone.  A constant real
+    slot vector (m(X) = c * Delta, the worst case for the coefficient bound)
+    is encrypted on two limbs, multiplied and rescaled by he_mul_rescale_batch
+    down to q0: a product below q0 / (2 * scale) decodes exactly, one above
+    it wraps modulo q0 -- the capacity is stated, not hidden."""
+    import ctypes
+    import torch
+    kind, kw = PARAMS["bench51"]
+    product.init_params(**kw)
+    product.set_seed(3)
+    pk, sk, _, rlk = keys(product, rot=False)
+    n, s, lvl = product.n, product.slots, 2
+    delta = product.info.delta
+    scale = delta * delta / product.primes[lvl - 1]
+    cap = product.primes[0] / 2 / scale
+    c = np.sqrt(frac * cap)
+    z = np.full(s, c, dtype=np.complex128)
+    h = product.export(product.encrypt(z, pk, nlimbs=lvl)).ravel()
+    da = torch.from_numpy(h.view(np.int64)).cuda()
+    dout = torch.zeros(2 * (lvl - 1) * n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.he_mul_rescale_batch(dout.data_ptr(), da.data_ptr(), da.data_ptr(), 1, lvl, ctypes.byref(rlk))
+    product.sync()
+    ct = product.ct()
+    product.import_(ct, dout.cpu().numpy().view(np.uint64), lvl - 1, scale=scale)
+    err = np.abs(product.decrypt(ct, sk) - c * c).max()
+    product.free(ct)
+    if ok:
+        assert err < 1e-6, err
+    else:
+        assert abs(err - product.primes[0] / scale) < 1e-3, (err, product.primes[0] / scale)
+
+
 @pytest.mark.parametrize("name,lvl,cnt", [("bench51", 6, 2), ("bench_d2", 3, 2), ("bench51", 8, 1),
                                           ("bench51", 8, 0)])
 def test_mul_rescale_batch_levels(oracle, product, name, lvl, cnt):
