@@ -20,6 +20,8 @@ for f in files:
         extra += f"  60-bit {d['value_60bit']:.0f}"
     if "config5" in d:
         extra += f"  c5 {d['config5']['value']:.0f}"
+        if "value_60bit" in d["config5"]:
+            extra += f"  c5-60bit {d['config5']['value_60bit']:.0f}"
     print(f"{os.path.basename(f):16s} {d['value']:9.0f} {d['unit']}{extra}  ms/step {d['ms_per_step']:.3f}")
     if "ntt_roundtrip" in d:
         t = d["ntt_roundtrip"]
