@@ -1871,7 +1871,7 @@ static const uint64_t *diag_pt(const double *diag, unsigned s, unsigned lvl)
 // -- they run with the step's later elementwise ops -- and the inner products
 // form the difference where they read x (gemv_inner_kernel), which saves the
 // step a launch.  src: a0, b0, a1, b1.
-static bool ew_lazy_sub(const he_ct_t *x, const uint64_t *src[4])
+static bool ew_lazy_sub(const he_ct_t *y, const he_ct_t *x, const uint64_t *src[4])
 {
   static const bool on = env_u("GPQHE_DEFER_SUB", 1);
   if (!g_pew.count || !on)
@@ -1897,6 +1897,17 @@ static bool ew_lazy_sub(const he_ct_t *x, const uint64_t *src[4])
   }
   if (!m0 || !m1)
     return false;
+  // the gemv then runs before these ops (flush_gemvs precedes the queued
+  // program): its output must not be an operand or output of any of them
+  // (in-place he_gemv, or y = an operand of a sub), nor of the pending gemvs'
+  // formed differences
+  const uint64_t *ylo = y->data, *yhi = y->data + 2 * pstride(y);
+  auto hits = [&](const uint64_t *p, unsigned lvl) { return p && p < yhi && p + ((size_t)lvl << G.logn) > ylo; };
+  for (unsigned j = 0; j < g_pew.count; j++) {
+    const EwOp &o = g_pew.op[j];
+    if (hits(o.out, o.lvl) || hits(o.a, o.lvl) || hits(o.b, o.lvl) || hits(o.s, o.lvl))
+      return false;
+  }
   src[0] = m0->a;
   src[1] = m0->b;
   src[2] = m1->a;
@@ -2035,7 +2046,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   // x may be a queued difference: left queued when the inner products can
   // form it (ew_lazy_sub, only with x's ModUp digits precomputed), else run
   const uint64_t *lz[4];
-  const bool lazy = ew_lazy_sub(x, lz);
+  const bool lazy = ew_lazy_sub(y, x, lz);
   if (!lazy)
     flush_ew();
   if (!g_pecd.empty() || !g_penc.empty())

@@ -2,8 +2,12 @@
 
 One process per GPU (torch.distributed; backend "nccl" = RCCL on ROCm, "gloo"
 for CPU tests).  Ciphertexts are independent, so there is no data-path
-collective: every rank holds a replica of the context and keys (same seed)
-and processes the pairs whose global index falls in its shard.  Collectives
+collective: every rank holds a replica of the context and keys generated from
+one seed (bench.py KEY_SEED), so all ranks work under one key, and processes
+the pairs whose global index falls in its shard (fill_pairs: pair g from seeds
+of g alone).  bench.py --check-shards gathers the product's output shards and
+compares them with one context's run of the whole global batch
+(tests/test_gpu_dist.py).  Collectives
 carry only the barrier, the max-over-ranks time and (tests) result gathers.
 """
 from __future__ import annotations

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Stall attribution of the headline pipeline's kernels: one SQ counter group
+# per rocprofv3 pass (no other tracing) over a short single-stream bench run,
+# plus the counter list of this box.   RUN=name bash scripts/gpu_stall.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${RUN:-stall}
+mkdir -p $OUT
+timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+B="python bench.py --steps 2 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --alt-bits 0 --streams 1 ${BENCH_ARGS}"
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
+           "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_VMEM SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_WAVES SQ_LEVEL_WAVES" \
+           ${EXTRA_GROUPS}; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d $OUT/p$i -o p$i --output-format csv -- $B > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python scripts/stall_summary.py $OUT > $OUT/summary.txt
+cat $OUT/summary.txt

@@ -1,0 +1,35 @@
+"""The N > 1 path on the product library: bench.py
+--gpus 2 starts its own two rank processes before anything touches the GPU,
+both on the one visible MI355X (gloo for the collectives: RCCL needs distinct
+devices), each multiplies its shard of one global batch at the headline shape
+(N=2^16, L=8, dnum=2, K=4) under one key (both ranks' key replicas come from
+the same seed), and rank 0 compares the gathered shards word for word with a
+single context's run of the whole global batch (bench.py --check-shards)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_bench_two_ranks_shards_bit_exact(streams):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
+           "1", "--streams", str(streams), "--no-cpu", "--no-cstr", "--no-ntt", "--no-c5", "--alt-bits", "0",
+           "--check-shards"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["batch_per_gpu"] == 3
+    chk = d["shard_check"]
+    assert chk["pairs"] == 6 and chk["ranks"] == 2
+    assert chk["bit_exact"], chk

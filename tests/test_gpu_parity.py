@@ -596,44 +596,10 @@ def test_speculative_encryption_noise(oracle, product):
     Steps of 5 encryptions (HECTR's), then 3 (a prefix of the speculated
     streams), 6 (more than speculated), one of a live plaintext, an
     encryption at a lower level, and a reseed between steps -- every
-    ciphertext bit-exact vs the oracle's sequential calls."""
-    init_both(oracle, product, "ref")
-    rng = np.random.default_rng(9)
-    plan = [5, 5, 3, 6, "live", "lvl1", "reseed", 5, 5]
-    zs = [[rng.uniform(-1, 1, oracle.slots) + 0j for _ in range(6)] for _ in plan]
-    out = {}
-    for e in (oracle, product):
-        pk, sk, _, _ = keys(e, rot=False)
-        res = []
-        for step, (kind, zz) in enumerate(zip(plan, zs)):
-            if kind == "reseed":
-                e.set_seed(77)
-                continue
-            cnt = kind if isinstance(kind, int) else 2
-            lvl = 1 if kind == "lvl1" else e.L
-            pts, cts = [], []
-            for z in zz[:cnt]:
-                pt = e.pt()
-                e.ecd_ex(pt, z, e.slots, e.info.delta, lvl)
-                pts.append(pt)
-            for pt in pts:
-                ct = e.ct()
-                e.enc_pk(ct, pt, pk)
-                cts.append(ct)
-            if kind == "live":
-                res.append(e.export(pts[0]))
-            for pt in pts:
-                e.free(pt)
-            d = e.ct()
-            e.sub(d, cts[0], cts[1])
-            res += [e.export(x) for x in cts + [d]]
-            res.append(e.decrypt(d, sk))  # he_dcd: the next step's noise is launched behind it
-            for x in cts + [d]:
-                e.free(x)
-        out[e.name] = res
-    assert len(out["oracle"]) == len(out["product"])
-    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
-        assert np.array_equal(x, y), f"object {i} differs"
+    ciphertext bit-exact vs the oracle's sequential calls
+    (tests/small_n_steps.py)."""
+    from tests.small_n_steps import mismatches, speculative_noise
+    assert mismatches(speculative_noise(oracle), speculative_noise(product)) == []
 
 
 def test_gemv_of_queued_differences(oracle, product):
@@ -644,46 +610,43 @@ def test_gemv_of_queued_differences(oracle, product):
     Variants per step: the differences freed unread (their queued subs are
     dropped), read back after the gemvs (the subs must still run), an operand
     of a sub overwritten after the gemvs (the gemv must see the old value),
-    and GPQHE-style non-speculated steps (a different number of encryptions)
-    -- every exported object and decoded value bit-exact vs the oracle."""
-    init_both(oracle, product, "ref")
-    rng = np.random.default_rng(31)
-    s = oracle.slots
-    M1 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
-    M2 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
-    plan = ["free", "free", "read", "free", "clobber", "free", "four", "free", "free"]
-    zs = [[rng.uniform(-1, 1, s) + 0j for _ in range(5)] for _ in plan]
-    out = {}
-    for e in (oracle, product):
-        pk, sk, rk, _ = keys(e, rot=True)
-        res = []
-        for kind, zz in zip(plan, zs):
-            cnt = 4 if kind == "four" else 5
-            cts = [e.encrypt(z, pk) for z in zz[:cnt]]
-            xd, ud = e.ct(), e.ct()
-            e.sub(xd, cts[0], cts[1])
-            e.sub(ud, cts[2], cts[3])
-            ya, yb = e.ct(), e.ct()
-            e.gemv(ya, M1.ravel(), xd, rk)
-            e.gemv(yb, M2.ravel(), ud, rk)
-            du = e.ct()
-            e.add(du, ya, yb)
-            e.neg(du)
-            if kind == "read":
-                res += [e.export(xd), e.export(ud)]
-            if kind == "clobber":
-                e.add(cts[0], cts[0], cts[1])  # an operand of the first sub
-                res.append(e.export(cts[0]))
-            res += [e.export(ya), e.export(yb), e.export(du)]
-            for x in (xd, ud, ya, yb):
-                e.free(x)
-            res.append(e.decrypt(du, sk))
-            for x in cts + [du]:
-                e.free(x)
-        out[e.name] = res
-    assert len(out["oracle"]) == len(out["product"])
-    for i, (x, y) in enumerate(zip(out["oracle"], out["product"])):
-        assert np.array_equal(x, y), f"object {i} differs"
+    GPQHE-style non-speculated steps (a different number of encryptions),
+    an in-place he_gemv(x, M, x) and a gemv whose output is an operand of the
+    queued sub (the lazy form must not run the gemv ahead of those subs:
+    ADVICE r3) -- every exported object and decoded value bit-exact vs the
+    oracle (tests/small_n_steps.py)."""
+    from tests.small_n_steps import mismatches, queued_differences
+    assert mismatches(queued_differences(oracle), queued_differences(product)) == []
+
+
+def test_rekey_between_speculative_steps(oracle, product):
+    """The speculative ModUp is keyed on the public key's block (api.cpp
+    SpecModup / C1Prov): re-keying between steps -- the key freed and a new
+    he_keypair that may take its block, then two keys alternating step by
+    step -- must never reuse digits made with another key's values; bit-exact
+    vs the oracle."""
+    from tests.small_n_steps import mismatches, rekeyed_steps
+    assert mismatches(rekeyed_steps(oracle), rekeyed_steps(product)) == []
+
+
+@pytest.mark.parametrize("switch", ["GPQHE_SPEC", "GPQHE_SPEC_ATTACH", "GPQHE_SPEC_EARLY", "GPQHE_DEFER",
+                                    "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV"])
+def test_small_n_switch_off_paths(switch):
+    """Each small-N switch is read once per process (api.cpp static const), so
+    its off path runs in a child process (one at a time, nothing else on the
+    GPU meanwhile): the three step sequences of tests/small_n_steps.py with
+    the switch at 0, bit-exact vs the oracle."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **{switch: "0"})
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "switch_worker.py")], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res == {k: [] for k in res} and len(res) == 3, res
 
 
 @pytest.mark.parametrize("name", ["ref", "c1"])
