@@ -1984,8 +1984,18 @@ static void flush_gemvs()
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 2, lvl, 1);
   else
     k_moddown(q[0].y, q[0].ypstride, acc.p, nm * n, 4, lvl, 1, q[1].y);
-  if (g_sa.sample || g_sa.ntt)
-    gpqhe_die("flush_gemvs: attached speculative work not taken (%d %d)", g_sa.sample, g_sa.ntt);
+  // spec_attach predicts which launches take the attached work; should a
+  // launch's own eligibility test (kernels.hip: gemv_inner's z slice, the
+  // ModDown's dropped limbs) ever disagree, the work runs here in its own
+  // launches, same streams and buffers, so the speculation stays valid
+  if (g_sa.sample) {
+    g_sa.sample = false;
+    k_sample_enc(g_sa.noise, g_sa.stream, g_sa.npoly);
+  }
+  if (g_sa.ntt) {
+    g_sa.ntt = false;
+    k_ntt(g_sa.noise, false);
+  }
 }
 
 // Unqueued he_gemv for matrices whose diagonals may overflow the cache: a

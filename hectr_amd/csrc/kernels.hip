@@ -15,6 +15,7 @@
 // with one 8-byte word per lane, canonical residues in and out.
 #include "gpqhe_internal.h"
 #include "ntt_device.h"
+#include "tables.h"
 
 #include <type_traits>
 
@@ -467,10 +468,16 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
   const double pass_bytes = 16.0 * n * s.count;
   // row pass: ntt_rows_q_kernel when every slot has polys enough to share
   // a workgroup's staged twiddles, else one tile per workgroup
+  // every limb of the set on an FP64 modulus: the LDS-twiddle column pass
+  bool allf = GPQHE_COLSF && G.twd != nullptr;
+  for (unsigned i = 0; i < s.per; i++)
+    allf &= G.q[s.mods[i]] < (1ull << 51);
   auto cols_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
     // (several tiles per workgroup with the next tile's words requested ahead
     // measured slower: 86 -> 103 us forward, 73 -> 88 us inverse per 48-poly group)
-    if (inv)
+    if (allf)
+      ntt2_colsf_launch(LOGT1, inv, blocks, in, out, post);
+    else if (inv)
       hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, true>), dim3(blocks), dim3(256), 0, G.stream, in, out, logn, tw,
                          G.dev.mc, post);
     else
@@ -1066,11 +1073,22 @@ __global__ void sample_enc_kernel(LimbSet dst, unsigned logn, ChachaKey key, uin
   }
 }
 
+// The noise alone (speculation, keygen paths): no 2.6 KB EncCoef argument to
+// copy into every launch
+__global__ void sample_noise_kernel(LimbSet dst, unsigned logn, ChachaKey key, uint64_t stream, const ModConst *mc)
+{
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < (1u << logn))
+    enc_noise_store(dst, logn, key, stream, mc, blockIdx.y, k);
+}
+
 void k_sample_enc(const LimbSet &dst, uint64_t stream, unsigned npoly, const EncCoef *ec)
 {
-  static const EncCoef none{};
-  hipLaunchKernelGGL(sample_enc_kernel, dim3((G.n + TPB - 1) / TPB, npoly), dim3(TPB), 0, G.stream, dst, G.logn,
-                     G.key, stream, G.dev.mc, ec ? *ec : none, ec ? 1 : 0);
+  const dim3 grid((G.n + TPB - 1) / TPB, npoly);
+  if (ec)
+    hipLaunchKernelGGL(sample_enc_kernel, grid, dim3(TPB), 0, G.stream, dst, G.logn, G.key, stream, G.dev.mc, *ec, 1);
+  else
+    hipLaunchKernelGGL(sample_noise_kernel, grid, dim3(TPB), 0, G.stream, dst, G.logn, G.key, stream, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1752,14 +1770,7 @@ void k_add_pt(uint64_t *out, const uint64_t *a, const uint64_t *pt, unsigned lvl
 // ===========================================================================
 // Basis conversion constants, cached per (kind, level) in device memory.
 // ===========================================================================
-// ModUp table for level lvl, digit j with limbs [lo, hi) (na = hi - lo):
-//   y[i] = [(Qj/q_i)^-1]_{q_i} (+ Shoup)     i in digit
-//   c[i][t] = [Qj/q_i]_{mod_t}               t in basis_qp(lvl)
-struct UpDigit {
-  uint32_t lo, na, pad0, pad1;
-  uint64_t y[8], yp[8];
-};
-
+// (UpTable / DownTable: tables.h)
 static unsigned basis_qp(unsigned lvl, unsigned *mods)
 {
   for (unsigned t = 0; t < lvl; t++)
@@ -1769,14 +1780,6 @@ static unsigned basis_qp(unsigned lvl, unsigned *mods)
   return lvl + G.K;
 }
 
-struct UpTable {
-  UpDigit *dig;   // [ndig]
-  uint64_t *c;    // [ndig][8][nm]  [Qj/q_i]_t 2^64 mod q_t (Montgomery form)
-  uint64_t *ysc;  // [lvl][2]       n^-1 [(Qj/q_i)^-1]_{q_i} + Shoup (folded into the INTT)
-  double *cd;     // [ndig][8][nm][2] ([Qj/q_i]_t, that / q_t) as doubles (FP64 conversion)
-  unsigned ndig, nm;
-  int f64;        // every modulus of the basis < 2^51 (and FP64 enabled): FP64 conversion
-};
 
 // Row length n2 of the fused kernels' 4-step split (n = n1 x n2).
 static unsigned ks_logn2()
@@ -2528,8 +2531,12 @@ static void ks_cols_stage(const uint64_t *y, uint64_t *T1, unsigned count, unsig
         hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
                            t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
       };
-      tab.f64 && FBC64_KS_INVC ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
-                               : go(ks_cols4_kernel<LOGT1, NT, true, false>);
+      if (tab.f64 && FBC64_KS_INVC && GPQHE_COLSF && LOGT1 <= 7)
+        ks_colsf_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, members,
+                        ngroups, tab, tw);
+      else
+        tab.f64 && FBC64_KS_INVC ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
+                                 : go(ks_cols4_kernel<LOGT1, NT, true, false>);
     } else if (G.alpha <= 4) {
       constexpr unsigned NT = 4;
       const unsigned members = (nm - na_min + NT - 1) / NT;
@@ -2643,6 +2650,82 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   });
 }
 
+// d2_rows_kernel for the split key switch (ysc) when every limb is on an FP64
+// modulus: a workgroup owns (limb, row tile) and a range of pairs; QN
+// 256-thread quarters stream their own pairs (the next pair's a1, b1 words
+// requested while the current one is transformed) and share the tile's
+// inverse twiddles, staged once in LDS as 8-byte entries (RowTw, the quotient
+// from the product: ArF64Row<., true>, as ntt_rows_q_kernel's inverse).  The
+// per-tile kernel fetched every twiddle from L2 at every round and waited on
+// one pair's loads at a time (sq_wait_any 0.49).  Same values: canonical
+// outputs of the same exact residue arithmetic.
+template <int LOGN2, int QN>
+__global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y, const uint64_t *a, const uint64_t *b,
+                                                                     size_t in_stride, size_t in_pstride,
+                                                                     unsigned logn, unsigned lvl, unsigned count,
+                                                                     unsigned members, Tw2 tw, const ModConst *mcs,
+                                                                     const uint64_t *ysc)
+{
+  using T = Row8<LOGN2>;
+  __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];
+  __shared__ __attribute__((aligned(16))) uint64_t rtw[RowTw<LOGN2>::ENTRIES];
+  const unsigned n1 = 1u << (logn - LOGN2), tiles = n1 / T::R;
+  unsigned grp, mi;  // group = (limb, tile) on one XCD; members = pair ranges
+  if (!xcd_group(members, lvl * tiles, grp, mi))
+    return;
+  const unsigned pb0 = (unsigned)(((size_t)mi * count) / members), pb1 = (unsigned)(((size_t)(mi + 1) * count) / members);
+  if (pb0 >= pb1)
+    return;
+  const unsigned limb = grp / tiles, tile = grp % tiles;
+  const double q = (double)mcs[limb].q, qinv = 1.0 / q;
+  const unsigned row0 = tile * T::R;
+  const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
+  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  uint64_t *lq = rt[qi];
+  const size_t o = (size_t)limb << (logn + 1);
+  RowTw<LOGN2>::template stage<true>(rtw, (const uint64_t *)(tw.invd + o), n1 + row0, threadIdx.x, 256 * QN);
+  ArF64 ar0{q, qinv, tw.fwdd + o, tw.invd + o, q < (double)F64_LAZY};
+  const auto ar = row_policy<LOGN2, true>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0), rtw);
+  const double sd = f64_from_u52(ysc[2 * limb]);
+  // this thread's 8 consecutive words 8 th + k: its round-C elements
+  auto fetch = [&](uint64_t (&A1)[8], uint64_t (&B1)[8], unsigned p) {
+    const ulonglong2 *pa = (const ulonglong2 *)(a + p * in_stride + in_pstride + off + 8 * th);
+    const ulonglong2 *pb = (const ulonglong2 *)(b + p * in_stride + in_pstride + off + 8 * th);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const ulonglong2 x = pa[i], z = pb[i];
+      A1[2 * i] = x.x;
+      A1[2 * i + 1] = x.y;
+      B1[2 * i] = z.x;
+      B1[2 * i + 1] = z.y;
+    }
+  };
+  unsigned p = pb0 + qi;
+  uint64_t nA[8], nB[8];
+  if (p < pb1)
+    fetch(nA, nB, p);
+  __syncthreads();  // the staged twiddles
+  for (; p < pb1; p += QN) {
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      // exact FP64 product of canonical residues, then times the ModUp factor
+      // s: |r| <= q/2 after the reduction, so with the recomputed s / q the
+      // quotient is off by < 1/2 + 0.75 q 2^-52: |r s - .| < 0.9 q
+      r[k] = f64_mulmod_h(f64_from_u52(nA[k]), f64_from_u52(nB[k]), q, qinv);
+      r[k] = f64_mulmod_h(f64_red(r[k], q, qinv), sd, q, qinv);
+    }
+    if (p + QN < pb1)
+      fetch(nA, nB, p + QN);  // the next pair's words, in flight meanwhile
+    wave_sync();              // the previous pair's rounds have finished with the LDS tile
+    rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
+    uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      ST_STREAM(ar.canon(r[k]), &yo[(row << LOGN2) + l + T::TA * k]);
+  }
+}
+
 bool k_ks_fused_ok()
 {
   return ntt2_ok() && G.alpha <= 8 && G.K <= 4;  // K <= 4: the fused ModDown drops at most 5 limbs
@@ -2656,6 +2739,20 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
 {
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned n = G.n;
+  bool allf = !cols && !d2 && G.twd != nullptr && GPQHE_D2Q;
+  for (unsigned i = 0; i < lvl; i++)
+    allf &= G.q[i] < (1ull << 51);
+  if (allf) {
+    // ~12 pairs per quarter stream, as the NTT batch's row pass
+    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * 3);
+    constexpr int QN = 2;
+    const unsigned groups = lvl * (n / 2048), members = std::max(1u, count / (12 * QN));
+    hipLaunchKernelGGL((d2_rows_q_kernel<LOGN2, QN>), dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream,
+                       ybuf, a, b, in_stride, in_pstride, G.logn, lvl, count, members, tw, G.dev.mc,
+                       (const uint64_t *)tab.ysc);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   {
     // reads a1, b1; writes its inverse row pass (and d2 when asked)
     ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * (d2 ? 4 : 3));
@@ -2736,27 +2833,6 @@ void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total)
                      G.logn, G.nmod, logn2, G.twd ? 1 : 0, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
-
-// ModDown table: divide by the product of the drop moduli (basis positions
-// [keep, nm)), keep basis positions [0, keep).
-struct DownTable {
-  uint64_t *ysc;     // [nd][2]     n^-1 [(Dprod/d)^-1]_d + Shoup (folded into the INTT)
-  uint64_t *y, *yp;  // [nd]        [(Dprod/d)^-1]_d
-  uint64_t *c;       // [nd][keep]  [Dprod/d]_t
-  uint64_t *dinv, *dinvp;  // [keep]  [Dprod^-1]_t
-  double *cd;        // [nd][keep][2] ([Dprod/d]_t, that / q_t) as doubles (FP64 conversion)
-  // Split key switch (mul_split_launch): the ModDown's constant factors folded
-  // into the relinearization key (ksq kernels, per basis slot) and into the
-  // conversion constants, so no kernel multiplies by them:
-  //   kept slot t:    key x [Dprod^-1]_t; conversion [Dprod/d]_t [Dprod^-1]_t = [d^-1]_t
-  //   dropped slot t: key x n^-1 [(Dprod/d)^-1]_d (the INTT's scale, ysc)
-  uint64_t *ksc;     // [nm]        key scale s_t
-  uint64_t *kps;     // [nm][2]     [P s_t]_t + Shoup (the P (d0, d1) term of q slots)
-  uint64_t *cf;      // [nd][keep]  [d^-1]_t (Montgomery form)
-  double *cdf;       // [nd][keep][2] ([d^-1]_t, that / q_t)
-  unsigned keep, nd;
-  int f64;           // every modulus < 2^51 (and FP64 enabled): FP64 conversion
-};
 
 static std::map<std::pair<unsigned, int>, DownTable> g_down;
 
@@ -3234,7 +3310,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
       // the next step's speculative transforms and ModUp ride along (g_sa)
       SpecNtt sn{};
       unsigned xn = 0;
-      if (g_sa.ntt) {
+      if (g_sa.ntt && !g_sa.sample) {  // (transforms only of noise already sampled in stream order)
         sn.s = g_sa.noise;
         xn = g_sa.noise.count;
         g_sa.ntt = false;
@@ -3559,7 +3635,10 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
                          conv, G.logn, lvl, G.L, members, ngroups, tab, tw, G.dev.mc);
     };
     if (pre) {
-      if (tab.f64 && FBC64_DN)
+      if (tab.f64 && FBC64_DN && GPQHE_COLSF)
+        dn_colsf_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), X, x_pstride, x_off, conv, lvl, members, ngroups, tab,
+                        tw);
+      else if (tab.f64 && FBC64_DN)
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true, true>) : go(dn_cols_kernel<LOGT1, NT, true, true, true>);
       else
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false, true>)

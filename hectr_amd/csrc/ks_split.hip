@@ -5,6 +5,12 @@
 
 #include <algorithm>
 
+// ksq_kernel<keep> on FP64 prime sets: loads issued one phase ahead (below);
+// -DKSQ_KEEP_PF=0 builds the load-before-use form (same-box A/B)
+#ifndef KSQ_KEEP_PF
+#define KSQ_KEEP_PF 2
+#endif
+
 // ===========================================================================
 // Key switch split at the ModDown boundary, key tile shared by quarter streams.
 //
@@ -163,7 +169,22 @@ __global__ void __launch_bounds__(256 * QN, 1)
             cvw[half][k] = cv[(row << LOGN2) + l + T::TA * k];
         }
       }
-      if (EARLY && jo < NDIG)
+      // KEEP_PF (kept slots, FP64): every load one phase ahead -- the first
+      // input half before the converted limb's row pass, the second input half
+      // and each conv half while the previous phase computes -- instead of
+      // each load right before its use (sq_wait_any 0.45)
+      constexpr int KPL = KEEP && ALLF ? KSQ_KEEP_PF : 0;  // 1: the first input half only
+      constexpr bool KPF = KPL >= 2;
+      uint64_t inw2[KPF ? 4 : 1][4], cva[KPF ? 8 : 1], cvb[KPF ? 8 : 1];
+      auto ld_cv = [&](uint64_t (&w)[KPF ? 8 : 1], int half) {
+        if constexpr (KPF) {
+          const uint64_t *cv = conv + (((size_t)(2 * p + half) * t_n + t) << logn) + toff;
+#pragma unroll
+          for (int k = 0; k < 8; k++)
+            w[k] = cv[(row << LOGN2) + l + T::TA * k];
+        }
+      };
+      if ((EARLY || KPL) && jo < NDIG)
         ld_in(0);
 #pragma unroll
       for (int u = 0; u < NX; u++) {
@@ -210,13 +231,29 @@ __global__ void __launch_bounds__(256 * QN, 1)
           const double Pd = f64_from_u52(kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            if (h || !EARLY)
+            if constexpr (KPF) {
+              if (h == 0) {  // the second half's words into their own registers
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                  const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4);
+                  const ulonglong2 w0 = v2[0], w1 = v2[1];
+                  inw2[a][0] = w0.x;
+                  inw2[a][1] = w0.y;
+                  inw2[a][2] = w1.x;
+                  inw2[a][3] = w1.y;
+                }
+              } else {
+                ld_cv(cva, 0);
+              }
+            } else if (h || !(EARLY || KPL)) {
               ld_in(h);
+            }
+            auto iw = [&](int a, int e) { return KPF && h ? inw2[KPF ? a : 0][e] : inw[a][e]; };
 #pragma unroll
             for (int e = 0; e < 4; e++) {
               const int k = 4 * h + e;
-              const double A0 = f64_from_u52(inw[0][e]), B0 = f64_from_u52(inw[1][e]);
-              const double A1 = f64_from_u52(inw[2][e]), B1 = f64_from_u52(inw[3][e]);
+              const double A0 = f64_from_u52(iw(0, e)), B0 = f64_from_u52(iw(1, e));
+              const double A1 = f64_from_u52(iw(2, e)), B1 = f64_from_u52(iw(3, e));
               const double eb = __longlong_as_double((long long)kl[2 * jo][256 * k + th]);
               const double ea = __longlong_as_double((long long)kl[2 * jo + 1][256 * k + th]);
               const double x = f64_mulmod_h(A1, B1, ar.q, ar.qinv);  // |x| < 1.5 q
@@ -264,9 +301,17 @@ __global__ void __launch_bounds__(256 * QN, 1)
           const unsigned poly = 2 * p + half;
           const uint64_t *cv = conv + (((size_t)poly * t_n + t) << logn) + toff;
           V r[8];
+          if constexpr (KPF) {
+            if (half == 0)
+              ld_cv(cvb, 1);  // the second half's conv words, in flight meanwhile
 #pragma unroll
-          for (int k = 0; k < 8; k++)
-            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
+            for (int k = 0; k < 8; k++)
+              r[k] = A::load_lazy(half ? cvb[k] : cva[k]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+              r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
+          }
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           // out = f D^-1 - NTTrows(conv D^-1): both factors already folded in

@@ -283,6 +283,83 @@ struct ArF64 {
   }
 };
 
+// ArF64 for the all-FP64 column passes (cols_f64.hip): the twiddles from an
+// LDS table holding entries [0, T) of the modulus' (w, w / q) table -- a T-row
+// column pass reads no others -- and the lazy-reduction choice fixed at
+// compile time, so a transform is straight-line code with no global loads.
+// Same stages as ArF64, so the same bits.
+// SB: a scheduling barrier after every forward stage, so the compiler does
+// not hoist all of a 16-element round's LDS twiddle reads (60 VGPRs) to its
+// start (the T = 256 ModDown columns then spill 20 B/lane; with it, none).
+template <int LE, bool SB>
+__device__ __forceinline__ void fwd_stages_fl(double (&x)[1 << LE], const double *__restrict__ twd, uint64_t bb,
+                                              int log_thi, double q, double qinv, bool lz)
+{
+  if constexpr (!SB) {
+    fwd_stages_f<LE>(x, twd, bb, log_thi, q, qinv, lz);
+  } else {
+    constexpr int E = 1 << LE;
+#pragma unroll
+    for (int s = 0; s < LE; s++) {
+      const uint64_t Bs = bb >> (log_thi - s + 1);
+      const int half = E >> (s + 1);
+      if (!(lz && (s & 1))) {
+#pragma unroll
+        for (int k = 0; k < E; k++)
+          if (!(k & half))
+            x[k] = f64_red(x[k], q, qinv);
+      }
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        if (k & half)
+          continue;
+        const uint64_t i2 = 2 * (Bs + (uint64_t)(k >> (LE - s)));
+        const double X = x[k];
+        const double T = f64_mulmod(x[k + half], twd[i2], twd[i2 + 1], q);
+        x[k] = X + T;
+        x[k + half] = X - T;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+template <bool LZ, bool SB = false>
+struct ArF64C : ArF64 {
+  const double *twl;  // LDS: [T][2]
+  template <int LE>
+  __device__ __forceinline__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    fwd_stages_fl<LE, SB>(x, twl, bb, log_thi, q, qinv, LZ);
+  }
+  template <int LE>
+  __device__ __forceinline__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  {
+    inv_stages_f<LE>(x, twl, bb, log_tlo, q, qinv, LZ);
+  }
+};
+
+template <bool LZ, bool SB = false>
+__device__ __forceinline__ ArF64C<LZ, SB> make_f64c(double q, const double *twl)
+{
+  ArF64C<LZ, SB> a;
+  a.q = q;
+  a.qinv = 1.0 / q;
+  a.tw = a.itw = nullptr;
+  a.lz = LZ;
+  a.twl = twl;
+  return a;
+}
+
+template <bool SB = false, class F>
+__device__ __forceinline__ void with_f64c(double q, const double *twl, F &&f)
+{
+  if (q < (double)(1ull << 50))
+    f(make_f64c<true, SB>(q, twl));
+  else
+    f(make_f64c<false, SB>(q, twl));
+}
+
 // FP64 fast basis conversion term y c mod q_t for canonical y < q_i < 2^51 and
 // a constant c < q_t < 2^51 with cq = fl(c / q_t): y c / q_t < 2^51, so the
 // quotient estimate is off by at most 1, |result| <= q_t and every
@@ -1037,6 +1114,28 @@ static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
 {
   return ((ngroups + 7) / 8) * 8 * members;
 }
+
+// The all-FP64 column kernels of the split key switch (cols_f64.hip), used in
+// place of ks_cols4_kernel<., 8, true, true> / dn_cols_kernel<., 8, ., true,
+// true> for column lengths 2^6, 2^7; -DGPQHE_COLSF=0 builds the old ones
+// (same-box A/B).
+#ifndef GPQHE_COLSF
+#define GPQHE_COLSF 1
+#endif
+// d2_rows_q_kernel (pair ranges per workgroup, staged twiddles) for the split
+// key switch's first pass on FP64 prime sets; -DGPQHE_D2Q=0: d2_rows_kernel
+#ifndef GPQHE_D2Q
+#define GPQHE_D2Q 1
+#endif
+struct UpTable;
+struct DownTable;
+void ks_colsf_launch(int logt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
+                     unsigned lvl, unsigned nm, unsigned ndig, unsigned members, unsigned ngroups, const UpTable &tab,
+                     const Tw2 &tw);
+void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, const LimbSet &out,
+                       const uint64_t *post);
+void dn_colsf_launch(int logt, dim3 grid, const uint64_t *X, size_t x_pstride, size_t x_off, uint64_t *conv,
+                     unsigned lvl, unsigned members, unsigned ngroups, const DownTable &tab, const Tw2 &tw);
 
 // Split key switch, kept / dropped basis slots (ks_split.hip): one launch of
 // ksq_kernel for row length 2^logn2 and ndig digits.
