@@ -10,6 +10,11 @@
 
 #include <type_traits>
 
+// ks_colsf_kernel: the next digit limb's words requested one step ahead
+#ifndef COLSF_PF
+#define COLSF_PF 1
+#endif
+
 // ---------------------------------------------------------------------------
 // The INVC ks_cols4 for every modulus below 2^51 (the headline's prime sets):
 // the same steps and values, scheduled so that no transform waits on a global
@@ -28,17 +33,25 @@
 //     butterfly code has no run-time branches.
 // (ks_cols4_kernel: every twiddle and constant by global load inside its
 // transform -- five L2 round trips per target.)
-template <int LOGT>
+// NT: targets per block (8; 12 when a digit has more than 8, config 5: its
+// column INTT then still runs once per digit tile).  T = 256 (n = 2^17): two
+// data tiles and three twiddle buffers would exceed the 80 KB two blocks per
+// CU allow, so a single tile with a barrier before every step and two twiddle
+// buffers (as dn_colsf_kernel), and scheduling barriers between the forward
+// stages (ArF64C SB: no spills).
+template <int LOGT, int NT>
 __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, size_t y_stride, uint64_t *T1,
                                                            size_t t1_stride, unsigned logn, unsigned lvl,
                                                            unsigned L, unsigned nm, unsigned ndig, unsigned members,
                                                            unsigned ngroups, UpTable tab, Tw2 tw,
                                                            const ModConst *mcs)
 {
-  constexpr int NT = 8, T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
+  constexpr int T = 1 << LOGT, C = 4096 / T, LEA = LOGT - 4, EA = 1 << LEA, CP = C + 1, IT = C / 16;
   constexpr int TWW = 2 * T, TWP = (TWW + 255) / 256;  // twiddle words per step, per thread
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2][T * CP];
-  __shared__ __attribute__((aligned(16))) double twl[3][TWW];
+  constexpr bool DB = LOGT <= 7;                        // double-buffered data tiles
+  constexpr int NB = DB ? 3 : 2;                        // twiddle buffers
+  __shared__ __attribute__((aligned(16))) uint64_t lds[DB ? 2 : 1][T * CP];
+  __shared__ __attribute__((aligned(16))) double twl[NB][TWW];
   __shared__ __attribute__((aligned(16))) double cst[NT][4][2];
   __shared__ double qs[4 + NT];
   __shared__ unsigned ord[NT];
@@ -72,7 +85,7 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
 #pragma unroll
     for (int w = 0; w < TWP; w++)
       if (th + 256 * w < TWW)
-        twl[z % 3][th + 256 * w] = tv[w];
+        twl[z % NB][th + 256 * w] = tv[w];
   };
   // targets run lazy moduli (q < 2^50) first, then the others: two loops with
   // the policy fixed at compile time (one loop choosing per target spilled
@@ -107,6 +120,19 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
     tw_load(1);
   const uint64_t *yb = ybuf + p * y_stride + ((size_t)lo << logn) + (size_t)tile * C;
   double y[IT][4][EA];
+  // round A words of digit limb i (16 rows of one column per thread); with
+  // COLSF_PF, limb i + 1's are requested while limb i is transformed (the
+  // registers of the limbs not yet converted are free then)
+  uint64_t pre[16];
+  auto ld_limb = [&](int i) {
+    const uint64_t *src = yb + ((size_t)i << logn);
+    const int c = th % C, g = th / C;
+    const unsigned vo = (unsigned)(16 * g) * n2 + c;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      pre[k] = (src + (size_t)k * n2)[vo];
+  };
+  ld_limb(0);
   // the digit arrives after the inverse row pass (d2_rows_kernel, which also
   // applied n^-1 [(Qj/q_i)^-1]): the inverse column pass, limb by limb
   auto invc = [&](auto I) {
@@ -119,17 +145,22 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
           y[it][i][k] = 0.0;
       return;
     }
-    uint64_t *buf = lds[i & 1];
-    const uint64_t *src = yb + ((size_t)i << logn);
-    with_f64c(qs[i], twl[i % 3], [&](const auto &ar) {
+    uint64_t *buf = lds[DB ? i & 1 : 0];
+    if (!COLSF_PF && i)
+      ld_limb(i);
+    if (!DB && i)
+      __syncthreads();  // the previous step's round B has read the tile
+    with_f64c<!DB>(qs[i], twl[i % NB], [&](const auto &ar) {
       {
-        const int c = th % C, g = th / C;
-        const unsigned vo = (unsigned)(16 * g) * n2 + c;
+        const int g = th / C;
         double r[16];
 #pragma unroll
         for (int k = 0; k < 16; k++)
-          r[k] = f64_from_u52((src + (size_t)k * n2)[vo]);
+          r[k] = f64_from_u52(pre[k]);
+        if (COLSF_PF && i + 1 < (int)na)
+          ld_limb(i + 1);
         ar.template inv<4>(r, T + 16 * g, 0);
+        const int c = th % C;
 #pragma unroll
         for (int k = 0; k < 16; k++)
           buf[(16 * g + k) * CP + c] = (uint64_t)__double_as_longlong(r[k]);
@@ -161,7 +192,7 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
   invc(std::integral_constant<int, 3>{});
   auto target = [&](unsigned v, auto LZ) {
     const unsigned z = na + v;
-    uint64_t *buf = lds[z & 1];
+    uint64_t *buf = lds[DB ? z & 1 : 0];
     uint64_t *out = T1 + p * t1_stride + (((size_t)j * nm + slot(ord[v])) << logn) + (size_t)tile * C;
     double cw[4], cq[4];
 #pragma unroll
@@ -170,6 +201,8 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
       cq[i] = cst[v][i][1];
     }
     const double q = qs[z];
+    if (!DB)
+      __syncthreads();  // the previous step's round B has read the tile
     [&](const auto &ar) {
 #pragma unroll
       for (int it = 0; it < IT; it++) {
@@ -201,7 +234,7 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
 #pragma unroll
       for (int k = 0; k < 16; k++)  // T1: read lazily by the row passes (the double itself)
         ST_STREAM((uint64_t)__double_as_longlong(r[k]), &(out + (size_t)k * n2)[vo]);
-    }(make_f64c<decltype(LZ)::value>(q, twl[z % 3]));
+    }(make_f64c<decltype(LZ)::value, !DB>(q, twl[z % NB]));
   };
   for (unsigned v = 0; v < nlz; v++)
     target(v, std::true_type{});
@@ -290,6 +323,16 @@ __global__ void __launch_bounds__(256, 2) dn_colsf_kernel(const uint64_t *X, siz
   // INTT scale folded into the key): the inverse column pass, limb by limb;
   // limbs 0..3 stay in registers
   double y[IT][4][EA];
+  uint64_t pre[16];  // round A words of drop limb d (COLSF_PF: requested one step ahead)
+  auto ld_limb = [&](int d) {
+    const uint64_t *src = yb + ((size_t)d << logn);
+    const int c = th % C, g = th / C;
+    const unsigned vo = (unsigned)(16 * g) * n2 + c;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      pre[k] = (src + (size_t)k * n2)[vo];
+  };
+  ld_limb(0);
   auto invc = [&](auto D) {
     constexpr int d = decltype(D)::value;
     if (d >= (int)nd) {
@@ -301,17 +344,19 @@ __global__ void __launch_bounds__(256, 2) dn_colsf_kernel(const uint64_t *X, siz
             y[it][d][k] = 0.0;
       return;
     }
-    const uint64_t *src = yb + ((size_t)d << logn);
+    if (d && !(COLSF_PF && d < 4))  // (the fifth limb is not prefetched: with
+      ld_limb(d);                    // four limbs held it spilled 52 B/lane)
     if (d)
       __syncthreads();  // the previous step's round B has read the tile
     with_f64c<(LOGT >= 8)>(qs[d], twl[d & 1], [&](const auto &ar) {
       {
         const int c = th % C, g = th / C;
-        const unsigned vo = (unsigned)(16 * g) * n2 + c;
         double r[16];
 #pragma unroll
         for (int k = 0; k < 16; k++)
-          r[k] = f64_from_u52((src + (size_t)k * n2)[vo]);
+          r[k] = f64_from_u52(pre[k]);
+        if (COLSF_PF && d + 1 < (int)nd && d + 1 < 4)
+          ld_limb(d + 1);  // the next drop limb's words, in flight meanwhile
         ar.template inv<4>(r, T + 16 * g, 0);
 #pragma unroll
         for (int k = 0; k < 16; k++)
@@ -524,24 +569,33 @@ void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, c
   }
 }
 
-template <int LOGT>
+template <int LOGT, int NT>
 static void ks_colsf_go(dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride, unsigned lvl,
                         unsigned nm, unsigned ndig, unsigned members, unsigned ngroups, const UpTable &tab,
                         const Tw2 &tw)
 {
-  hipLaunchKernelGGL(ks_colsf_kernel<LOGT>, grid, dim3(256), 0, G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L,
+  hipLaunchKernelGGL((ks_colsf_kernel<LOGT, NT>), grid, dim3(256), 0, G.stream, y, y_stride, T1, t1_stride, G.logn, lvl, G.L,
                      nm, ndig, members, ngroups, tab, tw, G.dev.mc);
 }
 
-void ks_colsf_launch(int logt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
+void ks_colsf_launch(int logt, int nt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
                      unsigned lvl, unsigned nm, unsigned ndig, unsigned members, unsigned ngroups, const UpTable &tab,
                      const Tw2 &tw)
 {
-  switch (logt) {
-  case 6: ks_colsf_go<6>(grid, y, y_stride, T1, t1_stride, lvl, nm, ndig, members, ngroups, tab, tw); break;
-  case 7: ks_colsf_go<7>(grid, y, y_stride, T1, t1_stride, lvl, nm, ndig, members, ngroups, tab, tw); break;
-  default: gpqhe_die("ks_colsf: column length 2^%d", logt);
-  }
+#define KSF(LT, N) ks_colsf_go<LT, N>(grid, y, y_stride, T1, t1_stride, lvl, nm, ndig, members, ngroups, tab, tw)
+  if (nt == 8 && logt == 6)
+    KSF(6, 8);
+  else if (nt == 8 && logt == 7)
+    KSF(7, 8);
+  else if (nt == 8 && logt == 8)
+    KSF(8, 8);
+  else if (nt == 12 && logt == 7)
+    KSF(7, 12);
+  else if (nt == 12 && logt == 8)
+    KSF(8, 12);
+  else
+    gpqhe_die("ks_colsf: column length 2^%d, %d targets", logt, nt);
+#undef KSF
 }
 
 template <int LOGT, bool X5>

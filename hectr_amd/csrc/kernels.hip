@@ -2505,6 +2505,15 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
   });
 }
 
+// ks_colsf_kernel takes the digit tile and all its targets (at most 12) when
+// every modulus is on FP64 and the row length is one it is built for
+static bool ks_colsf_ok(const UpTable &tab, unsigned lvl)
+{
+  const unsigned na_min = lvl - (tab.ndig - 1) * G.alpha;
+  return GPQHE_COLSF && FBC64_KS_INVC && tab.f64 && G.alpha <= 4 && G.logn >= 13 && G.logn <= 17 &&
+         tab.nm - na_min <= (G.logn >= 14 ? 12u : 8u);
+}
+
 // ModUp of d2 (its INTT finished here when invc) into T1 [count][ndig][nm]:
 // the digit's limbs converted to every other basis slot, forward column pass.
 template <int LOGT1>
@@ -2531,10 +2540,12 @@ static void ks_cols_stage(const uint64_t *y, uint64_t *T1, unsigned count, unsig
         hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, ngroups)), dim3(256), 0, G.stream, y, y_stride, T1,
                            t1_stride, G.logn, lvl, G.L, nm, ndig, members, ngroups, tab, tw, G.dev.mc);
       };
-      if (tab.f64 && FBC64_KS_INVC && GPQHE_COLSF && LOGT1 <= 7)
-        ks_colsf_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, members,
+      if (ks_colsf_ok(tab, lvl)) {
+        // up to 12 targets per block (the digit's column INTT once per tile)
+        const int nt = nm - na_min <= 8 ? 8 : 12;
+        ks_colsf_launch(LOGT1, nt, dim3(xcd_blocks(1, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, 1,
                         ngroups, tab, tw);
-      else
+      } else
         tab.f64 && FBC64_KS_INVC ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
                                  : go(ks_cols4_kernel<LOGT1, NT, true, false>);
     } else if (G.alpha <= 4) {
@@ -3723,7 +3734,9 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   if (nd > 5)
     gpqhe_die("split key switch: ModDown over %u moduli unsupported (max 5)", nd);
   const unsigned na_min = lvl - (ndig - 1) * G.alpha;
-  const bool invc = G.alpha <= 4 && nm - na_min <= 8;
+  // the column INTT inside the ModUp kernel: up to 8 targets per digit, or 12
+  // on the all-FP64 column kernel (config 5)
+  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl));
   // workspace: the caller's (k_mul_split_ws_words) or the pool's
   const bool own = !ws;
   if (own)

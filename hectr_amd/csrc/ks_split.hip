@@ -8,7 +8,14 @@
 // ksq_kernel<keep> on FP64 prime sets: loads issued one phase ahead (below);
 // -DKSQ_KEEP_PF=0 builds the load-before-use form (same-box A/B)
 #ifndef KSQ_KEEP_PF
-#define KSQ_KEEP_PF 2
+#define KSQ_KEEP_PF 0
+#endif
+// pair streams of ksq_kernel<drop> on FP64 prime sets (3: 168 VGPRs, 2: 256)
+#ifndef KSQ_DROP_QN
+#define KSQ_DROP_QN 3
+#endif
+#ifndef KSQ_KEEP_QN
+#define KSQ_KEEP_QN 3
 #endif
 
 // ===========================================================================
@@ -391,7 +398,9 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
-    if (allf)
+    if (allf && ((!keep_stage && KSQ_DROP_QN == 2) || (keep_stage && KSQ_KEEP_QN == 2)))
+      ksq_launch<LOGN2, 2, 2, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
+    else if (allf)
       ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
     else  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk, 60-bit set)
       ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,

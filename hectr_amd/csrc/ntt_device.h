@@ -1129,7 +1129,7 @@ static inline unsigned xcd_blocks(unsigned members, unsigned ngroups)
 #endif
 struct UpTable;
 struct DownTable;
-void ks_colsf_launch(int logt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
+void ks_colsf_launch(int logt, int nt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
                      unsigned lvl, unsigned nm, unsigned ndig, unsigned members, unsigned ngroups, const UpTable &tab,
                      const Tw2 &tw);
 void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, const LimbSet &out,
