@@ -2545,9 +2545,13 @@ static void ks_cols_stage(const uint64_t *y, uint64_t *T1, unsigned count, unsig
         const int nt = nm - na_min <= 8 ? 8 : 12;
         ks_colsf_launch(LOGT1, nt, dim3(xcd_blocks(1, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, 1,
                         ngroups, tab, tw);
-      } else
+      } else if (!tab.f64 && GPQHE_COLSM && nm - na_min <= NT && LOGT1 <= 7) {
+        ks_colsm_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, members,
+                        ngroups, tab, tw);
+      } else {
         tab.f64 && FBC64_KS_INVC ? go(ks_cols4_kernel<LOGT1, NT, true, true>)
                                  : go(ks_cols4_kernel<LOGT1, NT, true, false>);
+      }
     } else if (G.alpha <= 4) {
       constexpr unsigned NT = 4;
       const unsigned members = (nm - na_min + NT - 1) / NT;
@@ -3651,6 +3655,9 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
                         tw);
       else if (tab.f64 && FBC64_DN)
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true, true>) : go(dn_cols_kernel<LOGT1, NT, true, true, true>);
+      else if (GPQHE_COLSM && LOGT1 <= 7)  // (at T = 256 it spilled 92 B/lane: the old form)
+        dn_colsm_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), X, x_pstride, x_off, conv, lvl, members, ngroups, tab,
+                        tw);
       else
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, false, true>)
                     : go(dn_cols_kernel<LOGT1, NT, true, false, true>);

@@ -17,6 +17,10 @@
 #ifndef KSQ_KEEP_QN
 #define KSQ_KEEP_QN 3
 #endif
+// three-digit keys (config 5), kept slots: staged forward row twiddles
+#ifndef KSQ_C5_KEEP_LTW
+#define KSQ_C5_KEEP_LTW 1
+#endif
 
 // ===========================================================================
 // Key switch split at the ModDown boundary, key tile shared by quarter streams.
@@ -360,7 +364,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
   });
 }
 
-template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW>
+// (DROP_LTW: the dropped slots' form takes LTW too; false: it reads its
+// twiddles from L2 whatever LTW says, for keys whose tile leaves no room)
+template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW, bool DROP_LTW = LTW>
 static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
                        size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl,
                        unsigned nm, unsigned t_lo, unsigned t_n)
@@ -375,7 +381,7 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
     members++;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const size_t t1_stride = (size_t)NDIG * nm * n;
-  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, LTW>;
+  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, DROP_LTW>;
   hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, T1, t1_stride, d01, evkm,
                      dst, dst_pstride, conv, ksc, kps, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
                      members, t_lo, t_n, tw, G.dev.mc);
@@ -410,7 +416,13 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
     // 96 KB of key tile: two streams and the row twiddles from L2 (config 5:
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
-    if (allf)
+    if (allf && keep_stage && KSQ_C5_KEEP_LTW)
+      // the kept slots stage only the forward row twiddles (16 KB): 96 KB of
+      // key + two row tiles + those fit (the dropped slots' inverse ones too
+      // would not)
+      ksq_launch<LOGN2, 3, 2, true, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl,
+                                                 nm, t_lo, t_n);
+    else if (allf)
       ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                                            t_lo, t_n);
     else

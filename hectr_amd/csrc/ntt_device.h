@@ -1134,6 +1134,17 @@ void ks_colsf_launch(int logt, int nt, dim3 grid, const uint64_t *y, size_t y_st
                      const Tw2 &tw);
 void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, const LimbSet &out,
                        const uint64_t *post);
+// cols_mixed.hip: the same for prime sets mixing FP64 and wider integer
+// moduli (GPQHE_COLSM; replaces ks_cols4_kernel<., 8, true, false> and
+// dn_cols_kernel<., 8, ., false, true>)
+#ifndef GPQHE_COLSM
+#define GPQHE_COLSM 1
+#endif
+void ks_colsm_launch(int logt, dim3 grid, const uint64_t *y, size_t y_stride, uint64_t *T1, size_t t1_stride,
+                     unsigned lvl, unsigned nm, unsigned ndig, unsigned members, unsigned ngroups, const UpTable &tab,
+                     const Tw2 &tw);
+void dn_colsm_launch(int logt, dim3 grid, const uint64_t *X, size_t x_pstride, size_t x_off, uint64_t *conv,
+                     unsigned lvl, unsigned members, unsigned ngroups, const DownTable &tab, const Tw2 &tw);
 void dn_colsf_launch(int logt, dim3 grid, const uint64_t *X, size_t x_pstride, size_t x_off, uint64_t *conv,
                      unsigned lvl, unsigned members, unsigned ngroups, const DownTable &tab, const Tw2 &tw);
 
