@@ -257,6 +257,11 @@ def kernel_key(name):
     names: the base name, plus <drop>/<keep> for the two ksq_kernel stages
     (5th template argument KEEP)."""
     base = name.split("<")[0].split("(")[0].strip()
+    # the column / first-pass kernels' forms by prime set (cols_f64.hip,
+    # cols_mixed.hip, d2_rows_q_kernel) under the pipeline role they fill
+    base = {"ks_colsf_kernel": "ks_cols4_kernel", "ks_colsm_kernel": "ks_cols4_kernel",
+            "dn_colsf_kernel": "dn_cols_kernel", "dn_colsm_kernel": "dn_cols_kernel",
+            "d2_rows_q_kernel": "d2_rows_kernel"}.get(base, base)
     if base == "ksq_kernel" and "<" in name:
         args = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
         if args in (["keep"], ["drop"]):

@@ -351,10 +351,12 @@ __device__ __forceinline__ ArF64C<LZ, SB> make_f64c(double q, const double *twl)
   return a;
 }
 
-template <bool SB = false, class F>
+// ONE: every modulus on the non-lazy policy (one instantiation of f; the
+// non-lazy stages are exact for every q < 2^51)
+template <bool SB = false, int ONE = 0, class F>
 __device__ __forceinline__ void with_f64c(double q, const double *twl, F &&f)
 {
-  if (q < (double)(1ull << 50))
+  if (!ONE && q < (double)(1ull << 50))
     f(make_f64c<true, SB>(q, twl));
   else
     f(make_f64c<false, SB>(q, twl));
