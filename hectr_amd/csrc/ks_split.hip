@@ -21,6 +21,11 @@
 #ifndef KSQ_C5_KEEP_LTW
 #define KSQ_C5_KEEP_LTW 1
 #endif
+// three-digit keys, dropped slots: 2 = forward row twiddles staged (16 KB),
+// the inverse ones from L2; 0 = both from L2
+#ifndef KSQ_C5_DROP_LTW
+#define KSQ_C5_DROP_LTW 2
+#endif
 
 // ===========================================================================
 // Key switch split at the ModDown boundary, key tile shared by quarter streams.
@@ -51,7 +56,7 @@
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
 // ===========================================================================
-template <int LOGN2, int NDIG, int QN, bool ALLF, bool KEEP, bool LTW>
+template <int LOGN2, int NDIG, int QN, bool ALLF, bool KEEP, int LTW>
 __global__ void __launch_bounds__(256 * QN, 1)
     ksq_kernel(const uint64_t *T1, size_t t1_stride, D01Src d01, const uint64_t *evkm, uint64_t *dst,
                size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned logn,
@@ -64,8 +69,10 @@ __global__ void __launch_bounds__(256 * QN, 1)
   __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];    // row tile per quarter
   // LTW: the tile's row-pass twiddles (RowTw), read by every quarter: with
   // every modulus on FP64 (ALLF) as 8-byte entries (forward, and inverse for
-  // the dropped slots), else the forward ones as 16-byte entries
-  constexpr int TWW = !LTW ? 2 : (ALLF && KEEP) ? RowTw<LOGN2>::ENTRIES : 2 * RowTw<LOGN2>::ENTRIES;
+  // the dropped slots unless LTW == 2: those from L2), else the forward ones
+  // as 16-byte entries
+  constexpr bool GINV = ALLF && !KEEP && LTW == 2;
+  constexpr int TWW = !LTW ? 2 : (ALLF && (KEEP || GINV)) ? RowTw<LOGN2>::ENTRIES : 2 * RowTw<LOGN2>::ENTRIES;
   __shared__ __attribute__((aligned(16))) uint64_t rtw[TWW];
   const unsigned n1 = 1u << (logn - LOGN2);
   const unsigned tiles = n1 / T::R;
@@ -121,7 +128,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     constexpr bool W8 = LTW && ALLF;
     if constexpr (W8) {
       RowTw<LOGN2>::template stage<true>(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
-      if constexpr (!KEEP)  // the dropped slots' inverse row pass
+      if constexpr (!KEEP && !GINV)  // the dropped slots' inverse row pass
         RowTw<LOGN2>::template stage<true>(rtw + RowTw<LOGN2>::ENTRIES, (const uint64_t *)ar0.itw, n1 + row0,
                                            threadIdx.x, 256 * QN);
       __syncthreads();
@@ -131,8 +138,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
     }
     const auto ar = [&] {
       if constexpr (LTW)
-        return row_policy<LOGN2, W8>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
-                                     W8 && !KEEP ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
+        return row_policy<LOGN2, W8, GINV>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
+                                           W8 && !KEEP && !GINV ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
       else
         return ar0;
     }();
@@ -364,9 +371,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
   });
 }
 
-// (DROP_LTW: the dropped slots' form takes LTW too; false: it reads its
-// twiddles from L2 whatever LTW says, for keys whose tile leaves no room)
-template <int LOGN2, int NDIG, int QN, bool ALLF, bool LTW, bool DROP_LTW = LTW>
+// (DROP_LTW: the dropped slots' form of LTW; 0: it reads its twiddles from
+// L2, 2: the forward ones staged only, for keys whose tile leaves less room)
+template <int LOGN2, int NDIG, int QN, bool ALLF, int LTW, int DROP_LTW = LTW>
 static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
                        size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl,
                        unsigned nm, unsigned t_lo, unsigned t_n)
@@ -416,12 +423,11 @@ static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64
     // 96 KB of key tile: two streams and the row twiddles from L2 (config 5:
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
-    if (allf && keep_stage && KSQ_C5_KEEP_LTW)
-      // the kept slots stage only the forward row twiddles (16 KB): 96 KB of
-      // key + two row tiles + those fit (the dropped slots' inverse ones too
-      // would not)
-      ksq_launch<LOGN2, 3, 2, true, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl,
-                                                 nm, t_lo, t_n);
+    if (allf && (keep_stage ? KSQ_C5_KEEP_LTW != 0 : KSQ_C5_DROP_LTW != 0))
+      // the forward row twiddles staged (16 KB): 96 KB of key + two row tiles
+      // + those fit (the dropped slots' inverse ones too would not)
+      ksq_launch<LOGN2, 3, 2, true, 1, 2 * (KSQ_C5_DROP_LTW != 0)>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc,
+                                                                    kps, count, lvl, nm, t_lo, t_n);
     else if (allf)
       ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                                            t_lo, t_n);

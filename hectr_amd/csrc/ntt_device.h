@@ -423,7 +423,9 @@ struct RowTw {
 // so on moduli >= 2^50 the products are reduced every stage (inverse) and
 // every other stage (forward): |.| < 1.75 q throughout, exact; below 2^50
 // the lazy bounds of fwd_stages_f / inv_stages_f hold with room to spare.
-template <int LOGN2, bool W8 = false>
+// GINV: 8-byte forward entries staged, the inverse on the global table (for
+// kernels whose LDS leaves room for one direction only)
+template <int LOGN2, bool W8 = false, bool GINV = false>
 struct ArF64Row : ArF64 {
   RowTw<LOGN2> rt;
   const uint64_t *itl = nullptr;
@@ -474,7 +476,7 @@ struct ArF64Row : ArF64 {
   template <int LE>
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
-    if (!W8 && !itl) {  // (uniform) no staged inverse table: the global one
+    if (GINV || (!W8 && !itl)) {  // (uniform) no staged inverse table: the global one
       ArF64::inv<LE>(x, bb, log_tlo);
     } else {
       constexpr int E = 1 << LE;
@@ -544,18 +546,18 @@ struct ArIntRow : ArInt {
   }
 };
 
-template <int LOGN2, bool W8 = false>
-__device__ __forceinline__ ArF64Row<LOGN2, W8> row_policy(const ArF64 &a, const uint64_t *lds, int64_t rel,
-                                                          const uint64_t *ilds = nullptr)
+template <int LOGN2, bool W8 = false, bool GINV = false>
+__device__ __forceinline__ ArF64Row<LOGN2, W8, GINV> row_policy(const ArF64 &a, const uint64_t *lds, int64_t rel,
+                                                                const uint64_t *ilds = nullptr)
 {
-  ArF64Row<LOGN2, W8> r;
+  ArF64Row<LOGN2, W8, GINV> r;
   static_cast<ArF64 &>(r) = a;
   r.rt = RowTw<LOGN2>{lds, rel};
   r.itl = ilds;
   return r;
 }
 
-template <int LOGN2, bool W8 = false>
+template <int LOGN2, bool W8 = false, bool GINV = false>
 __device__ __forceinline__ ArIntRow<LOGN2> row_policy(const ArInt &a, const uint64_t *lds, int64_t rel,
                                                       const uint64_t * = nullptr)
 {
