@@ -23,6 +23,10 @@
 #endif
 // three-digit keys, dropped slots: 2 = forward row twiddles staged (16 KB),
 // the inverse ones from L2; 0 = both from L2
+// mixed prime sets: each arithmetic class's slot runs on its own kernel
+#ifndef KSQ_SPLIT_AR
+#define KSQ_SPLIT_AR 1
+#endif
 #ifndef KSQ_C5_DROP_LTW
 #define KSQ_C5_DROP_LTW 2
 #endif
@@ -56,13 +60,19 @@
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
 // ===========================================================================
-template <int LOGN2, int NDIG, int QN, bool ALLF, bool KEEP, int LTW>
+// AR: the slots' arithmetic -- 1 every modulus below 2^51 (FP64), 2 every one
+// integer, 0 chosen per slot at run time (both bodies in one kernel: its
+// registers are the larger body's, so mixed prime sets launch each class's
+// slot runs on their own kernel instead, KSQ_SPLIT_AR).  The slots are
+// [t_lo, t_lo + t_n); conv (kept slots) holds cv_n slots per poly.
+template <int LOGN2, int NDIG, int QN, int AR, bool KEEP, int LTW>
 __global__ void __launch_bounds__(256 * QN, 1)
     ksq_kernel(const uint64_t *T1, size_t t1_stride, D01Src d01, const uint64_t *evkm, uint64_t *dst,
                size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned logn,
                unsigned lvl, unsigned L, unsigned nm, unsigned nmod, unsigned alpha, unsigned count, unsigned members,
-               unsigned t_lo, unsigned t_n, Tw2 tw, const ModConst *mcs)
+               unsigned t_lo, unsigned t_n, unsigned cv_n, Tw2 tw, const ModConst *mcs)
 {
+  constexpr bool ALLF = AR == 1;
   using T = Row8<LOGN2>;
   constexpr int NX = KEEP ? NDIG - 1 : NDIG;  // converted limbs per slot at most
   __shared__ __attribute__((aligned(16))) uint64_t kl[2 * NDIG][2048];  // (b_j, a_j), order k 256 + th
@@ -88,7 +98,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
   const uint64_t q = mc.q, q2 = 2 * q;
   const unsigned row0 = tile * T::R;
   const size_t toff = (size_t)row0 << LOGN2;
-  const bool f64 = ALLF || (q < F64_QMAX && tw.fwdd);  // key words as plain doubles (to_mont_kernel)
+  const bool f64 = ALLF || (AR == 0 && q < F64_QMAX && tw.fwdd);  // key words as plain doubles (to_mont_kernel)
   const uint64_t sk = ksc[t];  // the folded ModDown factor of this slot
   for (unsigned idx = threadIdx.x; idx < 2 * NDIG * 2048; idx += 256 * QN) {
     const unsigned c = idx >> 11, w = idx & 2047;
@@ -120,7 +130,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     const uint64_t r = hi + mulhi64(lo * mc.qneg_inv, q) + (lo != 0);
     a = lazy_lt2q(a + r, q2);
   };
-  with_arith_t<ALLF>(q, m, logn, tw, [&](const auto &ar0) {
+  with_arith_ar<AR>(q, m, logn, tw, [&](const auto &ar0) {
     using A0 = std::decay_t<decltype(ar0)>;
     constexpr bool F = std::is_same<A0, ArF64>::value;
     // 8-byte entries (ALLF: A0 is ArF64); the kept slots' 16-byte forward
@@ -181,7 +191,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
       if constexpr (KEEP && EARLY) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          const uint64_t *cv = conv + (((size_t)(2 * p + half) * t_n + t) << logn) + toff;
+          const uint64_t *cv = conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff;
 #pragma unroll
           for (int k = 0; k < 8; k++)
             cvw[half][k] = cv[(row << LOGN2) + l + T::TA * k];
@@ -196,7 +206,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
       uint64_t inw2[KPF ? 4 : 1][4], cva[KPF ? 8 : 1], cvb[KPF ? 8 : 1];
       auto ld_cv = [&](uint64_t (&w)[KPF ? 8 : 1], int half) {
         if constexpr (KPF) {
-          const uint64_t *cv = conv + (((size_t)(2 * p + half) * t_n + t) << logn) + toff;
+          const uint64_t *cv = conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff;
 #pragma unroll
           for (int k = 0; k < 8; k++)
             w[k] = cv[(row << LOGN2) + l + T::TA * k];
@@ -317,7 +327,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           const unsigned poly = 2 * p + half;
-          const uint64_t *cv = conv + (((size_t)poly * t_n + t) << logn) + toff;
+          const uint64_t *cv = conv + (((size_t)poly * cv_n + t) << logn) + toff;
           V r[8];
           if constexpr (KPF) {
             if (half == 0)
@@ -373,10 +383,10 @@ __global__ void __launch_bounds__(256 * QN, 1)
 
 // (DROP_LTW: the dropped slots' form of LTW; 0: it reads its twiddles from
 // L2, 2: the forward ones staged only, for keys whose tile leaves less room)
-template <int LOGN2, int NDIG, int QN, bool ALLF, int LTW, int DROP_LTW = LTW>
+template <int LOGN2, int NDIG, int QN, int AR, int LTW, int DROP_LTW = LTW>
 static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, const uint64_t *evkm, uint64_t *dst,
-                       size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl,
-                       unsigned nm, unsigned t_lo, unsigned t_n)
+                       size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc, const uint64_t *kps, unsigned count,
+                       unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n, unsigned cv_n)
 {
   const unsigned n = G.n, groups = t_n * (n / 2048);
   // pair ranges of about 8 pairs per quarter stream (128 pairs at N=2^16:
@@ -388,54 +398,88 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
     members++;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const size_t t1_stride = (size_t)NDIG * nm * n;
-  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, ALLF, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, ALLF, false, DROP_LTW>;
+  auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, AR, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, AR, false, DROP_LTW>;
   hipLaunchKernelGGL(kern, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, T1, t1_stride, d01, evkm,
                      dst, dst_pstride, conv, ksc, kps, G.logn, lvl, G.L, nm, G.nmod, G.alpha, count,
-                     members, t_lo, t_n, tw, G.dev.mc);
+                     members, t_lo, t_n, cv_n, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
+// ar: the slots' arithmetic class (ksq_kernel AR)
 template <int LOGN2>
-static void ksq_dispatch(unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
+static void ksq_dispatch(unsigned ndig, int ar, bool keep_stage, const uint64_t *T1, const D01Src &d01,
                          const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv,
                          const uint64_t *ksc, const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo,
-                         unsigned t_n)
+                         unsigned t_n, unsigned cv_n)
 {
+#define KSQ_ARGS keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n, cv_n
   // LDS: the key tile (2 ndig x 16 KB) + 16 KB per quarter stream (+ 32 KB of
   // row twiddles where they fit) <= 160 KB
   switch (ndig) {
   case 1:
     // two streams (256 VGPRs); four (1024 threads, 128 VGPRs) spilled 58-193:
     // 68.2k -> 77.6k ct-mult/s at N=2^16, L=4, dnum=1 (same box)
-    ksq_launch<LOGN2, 1, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
+    ksq_launch<LOGN2, 1, 2, 0, 1>(KSQ_ARGS);
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
-    if (allf && ((!keep_stage && KSQ_DROP_QN == 2) || (keep_stage && KSQ_KEEP_QN == 2)))
-      ksq_launch<LOGN2, 2, 2, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
-    else if (allf)
-      ksq_launch<LOGN2, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
-    else  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk, 60-bit set)
-      ksq_launch<LOGN2, 2, 2, false, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
-                                           t_lo, t_n);
+    if (ar == 1 && ((!keep_stage && KSQ_DROP_QN == 2) || (keep_stage && KSQ_KEEP_QN == 2)))
+      ksq_launch<LOGN2, 2, 2, 1, 1>(KSQ_ARGS);
+    else if (ar == 1)
+      ksq_launch<LOGN2, 2, 3, 1, 1>(KSQ_ARGS);
+    else if (ar == 2)  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk)
+      ksq_launch<LOGN2, 2, 2, 2, 1>(KSQ_ARGS);
+    else
+      ksq_launch<LOGN2, 2, 2, 0, 1>(KSQ_ARGS);
     break;
   case 3:
     // 96 KB of key tile: two streams and the row twiddles from L2 (config 5:
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
-    if (allf && (keep_stage ? KSQ_C5_KEEP_LTW != 0 : KSQ_C5_DROP_LTW != 0))
+    if (ar == 1 && (keep_stage ? KSQ_C5_KEEP_LTW != 0 : KSQ_C5_DROP_LTW != 0))
       // the forward row twiddles staged (16 KB): 96 KB of key + two row tiles
       // + those fit (the dropped slots' inverse ones too would not)
-      ksq_launch<LOGN2, 3, 2, true, 1, 2 * (KSQ_C5_DROP_LTW != 0)>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc,
-                                                                    kps, count, lvl, nm, t_lo, t_n);
-    else if (allf)
-      ksq_launch<LOGN2, 3, 2, true, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
-                                           t_lo, t_n);
+      ksq_launch<LOGN2, 3, 2, 1, 1, 2 * (KSQ_C5_DROP_LTW != 0)>(KSQ_ARGS);
+    else if (ar == 1)
+      ksq_launch<LOGN2, 3, 2, 1, 0>(KSQ_ARGS);
+    else if (ar == 2)
+      ksq_launch<LOGN2, 3, 2, 2, 0>(KSQ_ARGS);
     else
-      ksq_launch<LOGN2, 3, 2, false, false>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
-                                            t_lo, t_n);
+      ksq_launch<LOGN2, 3, 2, 0, 0>(KSQ_ARGS);
     break;
   default: gpqhe_die("split key switch: %u digits", ndig);
+  }
+#undef KSQ_ARGS
+}
+
+// Slots [t_lo, t_lo + t_n) of one stage.  Mixed prime sets (FP64 and 60-bit
+// moduli) launch each run of same-class slots on its class's kernel
+// (KSQ_SPLIT_AR): the dropped slots' outputs are relative to t_lo, so a run
+// starting at a writes from dst + (a - t_lo) limbs; the kept slots' outputs
+// and conv are indexed by the absolute slot.
+template <int LOGN2>
+static void ksq_stage(unsigned ndig, bool allf, bool keep_stage, const uint64_t *T1, const D01Src &d01,
+                      const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
+                      const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
+{
+  if (allf || !KSQ_SPLIT_AR || ndig == 1) {
+    ksq_dispatch<LOGN2>(ndig, allf ? 1 : 0, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
+                        t_lo, t_n, t_n);
+    return;
+  }
+  auto cls = [&](unsigned t) {
+    const unsigned m = t < lvl ? t : G.L + (t - lvl);
+    return G.twd != nullptr && G.q[m] < (1ull << 51) ? 1 : 2;
+  };
+  for (unsigned a = t_lo; a < t_lo + t_n;) {
+    const int c = cls(a);
+    unsigned b = a + 1;
+    while (b < t_lo + t_n && cls(b) == c)
+      b++;
+    uint64_t *d = keep_stage ? dst : dst + ((size_t)(a - t_lo) << G.logn);
+    ksq_dispatch<LOGN2>(ndig, c, keep_stage, T1, d01, evkm, d, dst_pstride, conv, ksc, kps, count, lvl, nm, a, b - a,
+                        t_n);
+    a = b;
   }
 }
 
@@ -445,15 +489,15 @@ void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const ui
 {
 #ifdef KSQ_DEV  // analysis builds: the bench's instantiations only
   if (logn2 == 8 && ndig == 2 && allf) {
-    ksq_launch<8, 2, 3, true, true>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n);
+    ksq_launch<8, 2, 3, 1, 1>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n, t_n);
     return;
   }
   gpqhe_die("KSQ_DEV build");
 #else
   switch (logn2) {
-  case 7: ksq_dispatch<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
-  case 8: ksq_dispatch<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
-  case 9: ksq_dispatch<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
+  case 7: ksq_stage<7>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
+  case 8: ksq_stage<8>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
+  case 9: ksq_stage<9>(ndig, allf, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n); break;
   default: gpqhe_die("split key switch: row length 2^%u", logn2);
   }
 #endif

@@ -599,6 +599,19 @@ __device__ __forceinline__ void with_arith_t(uint64_t q, unsigned m, unsigned lo
   }
 }
 
+// The same by arithmetic class: AR 1 every modulus FP64, 2 every one integer
+// (the caller launched the slots of one class), 0 chosen per modulus.
+template <int AR, class F>
+__device__ __forceinline__ void with_arith_ar(uint64_t q, unsigned m, unsigned logn, const Tw2 &tw, F &&f)
+{
+  if constexpr (AR == 2) {
+    const size_t o = (size_t)m << (logn + 1);
+    f(ArInt{q, tw.fwd + o, tw.inv + o});
+  } else {
+    with_arith_t<AR == 1>(q, m, logn, tw, f);
+  }
+}
+
 // Row-tile LDS swizzle: column c of a row lives at c ^ ((c >> 4) & 15).  Round
 // B reads 16 consecutive columns per thread at a 16-column lane stride; the
 // XOR spreads those lanes over distinct banks (8-way conflict without it).
