@@ -23,6 +23,13 @@
 #endif
 // three-digit keys, dropped slots: 2 = forward row twiddles staged (16 KB),
 // the inverse ones from L2; 0 = both from L2
+// FP64 slots: one kernel per lazy-reduction policy (AR 3 / 4), the slots
+// launched in runs of one policy; 0: the policy chosen per slot at run time
+// (AR 1), which the compiler if-converts -- both reductions computed, one
+// selected -- so every slot paid the non-lazy cost
+#ifndef KSQ_LZ_CT
+#define KSQ_LZ_CT 0
+#endif
 // mixed prime sets: each arithmetic class's slot runs on its own kernel
 #ifndef KSQ_SPLIT_AR
 #define KSQ_SPLIT_AR 1
@@ -60,7 +67,22 @@
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
 // ===========================================================================
-// AR: the slots' arithmetic -- 1 every modulus below 2^51 (FP64), 2 every one
+// the policy with its lazy-reduction choice fixed (LZ 0 / 1; -1 as it is)
+template <int LZ>
+__device__ __forceinline__ ArF64 with_lz(ArF64 a)
+{
+  if constexpr (LZ >= 0)
+    a.lz = LZ != 0;
+  return a;
+}
+template <int LZ>
+__device__ __forceinline__ ArInt with_lz(const ArInt &a)
+{
+  return a;
+}
+
+// AR: the slots' arithmetic -- 1 every modulus below 2^51 (FP64; 3 / 4: and
+// every one below / above 2^50, the lazy-reduction policy fixed), 2 every one
 // integer, 0 chosen per slot at run time (both bodies in one kernel: its
 // registers are the larger body's, so mixed prime sets launch each class's
 // slot runs on their own kernel instead, KSQ_SPLIT_AR).  The slots are
@@ -72,7 +94,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
                unsigned lvl, unsigned L, unsigned nm, unsigned nmod, unsigned alpha, unsigned count, unsigned members,
                unsigned t_lo, unsigned t_n, unsigned cv_n, Tw2 tw, const ModConst *mcs)
 {
-  constexpr bool ALLF = AR == 1;
+  constexpr bool ALLF = AR == 1 || AR >= 3;
   using T = Row8<LOGN2>;
   constexpr int NX = KEEP ? NDIG - 1 : NDIG;  // converted limbs per slot at most
   __shared__ __attribute__((aligned(16))) uint64_t kl[2 * NDIG][2048];  // (b_j, a_j), order k 256 + th
@@ -146,12 +168,19 @@ __global__ void __launch_bounds__(256 * QN, 1)
       RowTw<LOGN2>::stage(rtw, (const uint64_t *)ar0.tw, n1 + row0, threadIdx.x, 256 * QN);
       __syncthreads();
     }
+    // the pair loop, with the FP64 lazy-reduction choice as a compile-time
+    // constant (lzc: 1 / 0, -1 integer or run-time)
+    auto pairs = [&](auto lzc) {
+    constexpr int LZ = decltype(lzc)::value;
     const auto ar = [&] {
-      if constexpr (LTW)
-        return row_policy<LOGN2, W8, GINV>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
-                                           W8 && !KEEP && !GINV ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
-      else
-        return ar0;
+      if constexpr (LTW && F) {
+        return row_policy<LOGN2, W8, GINV, LZ>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0),
+                                               W8 && !KEEP && !GINV ? rtw + RowTw<LOGN2>::ENTRIES : nullptr);
+      } else if constexpr (LTW) {
+        return row_policy<LOGN2>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0));
+      } else {
+        return with_lz<LZ>(ar0);
+      }
     }();
     using A = std::decay_t<decltype(ar)>;
     using V = typename A::V;
@@ -378,6 +407,11 @@ __global__ void __launch_bounds__(256 * QN, 1)
         }
       }
     }
+    };
+    // (run-time choice: one branch per transform call for the kept slots,
+    // 1811 vs 1831 us per chunk; per element for the dropped ones, whose
+    // registers the branch form spills: 1196 vs 1258)
+    pairs(std::integral_constant<int, !F ? -1 : AR < 3 ? (KEEP ? -1 : -2) : AR == 3 ? 1 : 0>{});
   });
 }
 
@@ -405,6 +439,22 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
   HIP_CHECK(hipGetLastError());
 }
 
+// f(integral_constant<AR>) for an FP64 class: 3 / 4 (KSQ_LZ_CT) or 1
+template <class F>
+static void with_f64_class(int ar, F &&f)
+{
+  if constexpr (KSQ_LZ_CT) {
+    if (ar == 3)
+      f(std::integral_constant<int, 3>{});
+    else if (ar == 4)
+      f(std::integral_constant<int, 4>{});
+    else
+      gpqhe_die("split key switch: FP64 class %d", ar);
+  } else {
+    f(std::integral_constant<int, 1>{});
+  }
+}
+
 // ar: the slots' arithmetic class (ksq_kernel AR)
 template <int LOGN2>
 static void ksq_dispatch(unsigned ndig, int ar, bool keep_stage, const uint64_t *T1, const D01Src &d01,
@@ -423,10 +473,14 @@ static void ksq_dispatch(unsigned ndig, int ar, bool keep_stage, const uint64_t 
     break;
   case 2:
     // (four streams for the kept slots, 128 VGPRs: 36.4k vs 38.1k ct-mult/s)
-    if (ar == 1 && ((!keep_stage && KSQ_DROP_QN == 2) || (keep_stage && KSQ_KEEP_QN == 2)))
-      ksq_launch<LOGN2, 2, 2, 1, 1>(KSQ_ARGS);
-    else if (ar == 1)
-      ksq_launch<LOGN2, 2, 3, 1, 1>(KSQ_ARGS);
+    if (ar == 1 || ar >= 3)
+      with_f64_class(ar, [&](auto arc) {
+        constexpr int A = decltype(arc)::value;
+        if ((!keep_stage && KSQ_DROP_QN == 2) || (keep_stage && KSQ_KEEP_QN == 2))
+          ksq_launch<LOGN2, 2, 2, A, 1>(KSQ_ARGS);
+        else
+          ksq_launch<LOGN2, 2, 3, A, 1>(KSQ_ARGS);
+      });
     else if (ar == 2)  // integer moduli: two streams, 256 VGPRs (three spilled 180: drop 2.60 -> 1.78 ms per chunk)
       ksq_launch<LOGN2, 2, 2, 2, 1>(KSQ_ARGS);
     else
@@ -436,12 +490,16 @@ static void ksq_dispatch(unsigned ndig, int ar, bool keep_stage, const uint64_t 
     // 96 KB of key tile: two streams and the row twiddles from L2 (config 5:
     // 7.76k vs 7.51k ct-mult/s for the streaming ks_rows form; one stream with
     // staged twiddles 7.50k, same box)
-    if (ar == 1 && (keep_stage ? KSQ_C5_KEEP_LTW != 0 : KSQ_C5_DROP_LTW != 0))
-      // the forward row twiddles staged (16 KB): 96 KB of key + two row tiles
-      // + those fit (the dropped slots' inverse ones too would not)
-      ksq_launch<LOGN2, 3, 2, 1, 1, 2 * (KSQ_C5_DROP_LTW != 0)>(KSQ_ARGS);
-    else if (ar == 1)
-      ksq_launch<LOGN2, 3, 2, 1, 0>(KSQ_ARGS);
+    if (ar == 1 || ar >= 3)
+      with_f64_class(ar, [&](auto arc) {
+        constexpr int A = decltype(arc)::value;
+        if (keep_stage ? KSQ_C5_KEEP_LTW != 0 : KSQ_C5_DROP_LTW != 0)
+          // the forward row twiddles staged (16 KB): 96 KB of key + two row
+          // tiles + those fit (the dropped slots' inverse ones too would not)
+          ksq_launch<LOGN2, 3, 2, A, 1, 2 * (KSQ_C5_DROP_LTW != 0)>(KSQ_ARGS);
+        else
+          ksq_launch<LOGN2, 3, 2, A, 0>(KSQ_ARGS);
+      });
     else if (ar == 2)
       ksq_launch<LOGN2, 3, 2, 2, 0>(KSQ_ARGS);
     else
@@ -462,14 +520,16 @@ static void ksq_stage(unsigned ndig, bool allf, bool keep_stage, const uint64_t 
                       const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
                       const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
 {
-  if (allf || !KSQ_SPLIT_AR || ndig == 1) {
+  if ((allf && !KSQ_LZ_CT) || (!allf && !KSQ_SPLIT_AR) || ndig == 1) {
     ksq_dispatch<LOGN2>(ndig, allf ? 1 : 0, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                         t_lo, t_n, t_n);
     return;
   }
   auto cls = [&](unsigned t) {
     const unsigned m = t < lvl ? t : G.L + (t - lvl);
-    return G.twd != nullptr && G.q[m] < (1ull << 51) ? 1 : 2;
+    if (!(G.twd != nullptr && G.q[m] < (1ull << 51)))
+      return 2;
+    return !KSQ_LZ_CT ? 1 : G.q[m] < (1ull << 50) ? 3 : 4;
   };
   for (unsigned a = t_lo; a < t_lo + t_n;) {
     const int c = cls(a);

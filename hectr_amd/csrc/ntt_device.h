@@ -425,10 +425,14 @@ struct RowTw {
 // the lazy bounds of fwd_stages_f / inv_stages_f hold with room to spare.
 // GINV: 8-byte forward entries staged, the inverse on the global table (for
 // kernels whose LDS leaves room for one direction only)
-template <int LOGN2, bool W8 = false, bool GINV = false>
+template <int LOGN2, bool W8 = false, bool GINV = false, int LZC = -1>
 struct ArF64Row : ArF64 {
   RowTw<LOGN2> rt;
   const uint64_t *itl = nullptr;
+  // LZC: the lazy-reduction choice -- 0 / 1 at compile time, -1 one uniform
+  // branch per call (fwd / inv below), -2 per element at run time (which the
+  // compiler if-converts: both reductions computed, one selected, so every
+  // modulus pays the wide one; fewer registers than -1 in some kernels)
   __device__ __forceinline__ double2 twf(const uint64_t *tab, uint64_t e) const
   {
     if constexpr (W8) {
@@ -438,16 +442,42 @@ struct ArF64Row : ArF64 {
       return ((const double2 *)tab)[e];
     }
   }
+  // The lazy-reduction choice is made once per call (LZ below), not per
+  // element: a run-time lz inside the stages is if-converted (both
+  // reductions computed, one selected), so every modulus paid the wide one.
   template <int LE>
-  __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  __device__ __forceinline__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
+  {
+    if constexpr (LZC != -1)
+      fwd_p<LE, LZC>(x, bb, log_thi);
+    else if (lz)
+      fwd_p<LE, 1>(x, bb, log_thi);
+    else
+      fwd_p<LE, 0>(x, bb, log_thi);
+  }
+  template <int LE>
+  __device__ __forceinline__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  {
+    if (GINV || (!W8 && !itl))  // (uniform) no staged inverse table: the global one
+      ArF64::inv<LE>(x, bb, log_tlo);
+    else if constexpr (LZC != -1)
+      inv_p<LE, LZC>(x, bb, log_tlo);
+    else if (lz)
+      inv_p<LE, 1>(x, bb, log_tlo);
+    else
+      inv_p<LE, 0>(x, bb, log_tlo);
+  }
+  template <int LE, int LZM>
+  __device__ __forceinline__ void fwd_p(V (&x)[1 << LE], uint64_t bb, int log_thi) const
   {
     constexpr int E = 1 << LE;
+    const bool LZ = LZM < 0 ? lz : LZM != 0;
 #pragma unroll
     for (int s = 0; s < LE; s++) {
       const int shift = log_thi - s + 1;
       const uint64_t Bs = bb >> shift;
       const int half = E >> (s + 1);
-      if (!(lz && (s & 1))) {  // lazy reduction: see fwd_stages_f
+      if (!(LZ && (s & 1))) {  // lazy reduction: see fwd_stages_f
 #pragma unroll
         for (int k = 0; k < E; k++)
           if (!(k & half))
@@ -466,19 +496,18 @@ struct ArF64Row : ArF64 {
           const double2 w = twf(rt.lds, e);
           T = f64_mulmod(x[k + half], w.x, w.y, q);
         }
-        if (W8 && !lz && (s & 1))
+        if (W8 && !LZ && (s & 1))
           T = f64_red(T, q, qinv);  // recomputed w/q on a wide modulus: see below
         x[k] = X + T;
         x[k + half] = X - T;
       }
     }
   }
-  template <int LE>
-  __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
+  template <int LE, int LZM>
+  __device__ __forceinline__ void inv_p(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
-    if (GINV || (!W8 && !itl)) {  // (uniform) no staged inverse table: the global one
-      ArF64::inv<LE>(x, bb, log_tlo);
-    } else {
+    const bool LZ = LZM < 0 ? lz : LZM != 0;
+    {
       constexpr int E = 1 << LE;
 #pragma unroll
       for (int s = 0; s < LE; s++) {
@@ -498,16 +527,16 @@ struct ArF64Row : ArF64 {
             const double2 w = twf(itl, e);
             x[k + half] = f64_mulmod(U - V_, w.x, w.y, q);
           }
-          if (W8 && !lz)  // recomputed w/q on a wide modulus: see above
+          if (W8 && !LZ)  // recomputed w/q on a wide modulus: see above
             x[k + half] = f64_red(x[k + half], q, qinv);
         }
-        if (!(lz && (s & 1))) {  // lazy reduction: see inv_stages_f
+        if (!(LZ && (s & 1))) {  // lazy reduction: see inv_stages_f
 #pragma unroll
           for (int k = 0; k < E; k++)
             if (!(k & half))
               x[k] = f64_red(x[k], q, qinv);
         }
-        if (!W8 && !lz && s == LE - 1) {  // wide moduli: bounded products, see inv_stages_f
+        if (!W8 && !LZ && s == LE - 1) {  // wide moduli: bounded products, see inv_stages_f
 #pragma unroll
           for (int k = 0; k < E; k++)
             if (k & half)
@@ -546,12 +575,14 @@ struct ArIntRow : ArInt {
   }
 };
 
-template <int LOGN2, bool W8 = false, bool GINV = false>
-__device__ __forceinline__ ArF64Row<LOGN2, W8, GINV> row_policy(const ArF64 &a, const uint64_t *lds, int64_t rel,
-                                                                const uint64_t *ilds = nullptr)
+template <int LOGN2, bool W8 = false, bool GINV = false, int LZC = -1>
+__device__ __forceinline__ ArF64Row<LOGN2, W8, GINV, LZC> row_policy(const ArF64 &a, const uint64_t *lds, int64_t rel,
+                                                                     const uint64_t *ilds = nullptr)
 {
-  ArF64Row<LOGN2, W8, GINV> r;
+  ArF64Row<LOGN2, W8, GINV, LZC> r;
   static_cast<ArF64 &>(r) = a;
+  if constexpr (LZC >= 0)
+    r.lz = LZC != 0;  // (the base class's global-table passes see the constant)
   r.rt = RowTw<LOGN2>{lds, rel};
   r.itl = ilds;
   return r;
@@ -608,7 +639,7 @@ __device__ __forceinline__ void with_arith_ar(uint64_t q, unsigned m, unsigned l
     const size_t o = (size_t)m << (logn + 1);
     f(ArInt{q, tw.fwd + o, tw.inv + o});
   } else {
-    with_arith_t<AR == 1>(q, m, logn, tw, f);
+    with_arith_t<AR == 1 || AR >= 3>(q, m, logn, tw, f);
   }
 }
 
