@@ -2312,7 +2312,9 @@ static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inver
   // Infinity Cache when its row pass reads it (config 2, 1024 polys x 8 limbs
   // at N=2^16: roundtrip 8.41 -> 7.84 ms; 32-64 MiB groups lose more to
   // launch gaps than they gain)
-  const size_t per = std::max<size_t>(1, std::min<size_t>(65535 / nlimbs, ((size_t)192 << 20) /
+  // (GPQHE_NTT_GROUP_MIB: the group size for sweeps)
+  static const size_t group_mib = env_u("GPQHE_NTT_GROUP_MIB", 192);
+  const size_t per = std::max<size_t>(1, std::min<size_t>(65535 / nlimbs, (group_mib << 20) /
                                                                               ((size_t)nlimbs * G.n * 8)));
   for (size_t p0 = 0; p0 < npolys; p0 += per) {
     const unsigned cnt = (unsigned)std::min(per, npolys - p0);
