@@ -2507,6 +2507,13 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
 
 // ks_colsf_kernel takes the digit tile and all its targets (at most 12) when
 // every modulus is on FP64 and the row length is one it is built for
+// the mixed-set column kernel for `targets` targets per digit at T = 2^LOGT1
+template <int LOGT1>
+static bool colsm_ks_ok(unsigned targets)
+{
+  return GPQHE_COLSM && ((targets <= 8 && LOGT1 <= 7) || (GPQHE_COLSM_MB && LOGT1 <= 8));
+}
+
 static bool ks_colsf_ok(const UpTable &tab, unsigned lvl)
 {
   const unsigned na_min = lvl - (tab.ndig - 1) * G.alpha;
@@ -2545,7 +2552,7 @@ static void ks_cols_stage(const uint64_t *y, uint64_t *T1, unsigned count, unsig
         const int nt = nm - na_min <= 8 ? 8 : 12;
         ks_colsf_launch(LOGT1, nt, dim3(xcd_blocks(1, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, 1,
                         ngroups, tab, tw);
-      } else if (!tab.f64 && GPQHE_COLSM && nm - na_min <= NT && LOGT1 <= 7) {
+      } else if (!tab.f64 && colsm_ks_ok<LOGT1>(nm - na_min)) {
         ks_colsm_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), y, y_stride, T1, t1_stride, lvl, nm, ndig, members,
                         ngroups, tab, tw);
       } else {
@@ -3655,7 +3662,7 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
                         tw);
       else if (tab.f64 && FBC64_DN)
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true, true>) : go(dn_cols_kernel<LOGT1, NT, true, true, true>);
-      else if (GPQHE_COLSM && LOGT1 <= 7)  // (at T = 256 it spilled 92 B/lane: the old form)
+      else if (GPQHE_COLSM && (LOGT1 <= 7 || GPQHE_COLSM_DN8))  // (T = 256: 92 B/lane of spills, GPQHE_COLSM_DN8)
         dn_colsm_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), X, x_pstride, x_off, conv, lvl, members, ngroups, tab,
                         tw);
       else
@@ -3743,7 +3750,7 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   const unsigned na_min = lvl - (ndig - 1) * G.alpha;
   // the column INTT inside the ModUp kernel: up to 8 targets per digit, or 12
   // on the all-FP64 column kernel (config 5)
-  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl));
+  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl) || (!up.f64 && colsm_ks_ok<LOGT1>(nm - na_min)));
   // workspace: the caller's (k_mul_split_ws_words) or the pool's
   const bool own = !ws;
   if (own)

@@ -30,6 +30,10 @@
 #ifndef KSQ_LZ_CT
 #define KSQ_LZ_CT 0
 #endif
+// the dropped slots' run-time lazy choice (ArF64Row LZC: -2 per element)
+#ifndef KSQ_DROP_LZM
+#define KSQ_DROP_LZM -2
+#endif
 // mixed prime sets: each arithmetic class's slot runs on its own kernel
 #ifndef KSQ_SPLIT_AR
 #define KSQ_SPLIT_AR 1
@@ -411,7 +415,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     // (run-time choice: one branch per transform call for the kept slots,
     // 1811 vs 1831 us per chunk; per element for the dropped ones, whose
     // registers the branch form spills: 1196 vs 1258)
-    pairs(std::integral_constant<int, !F ? -1 : AR < 3 ? (KEEP ? -1 : -2) : AR == 3 ? 1 : 0>{});
+    pairs(std::integral_constant<int, !F ? -1 : AR < 3 ? (KEEP ? -1 : KSQ_DROP_LZM) : AR == 3 ? 1 : 0>{});
   });
 }
 

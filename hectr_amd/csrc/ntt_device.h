@@ -212,6 +212,10 @@ __device__ __forceinline__ void inv_stages_f(double (&x)[1 << LE], const double 
   }
 }
 
+#ifndef F64_LZ_CALL
+#define F64_LZ_CALL 1
+#endif
+
 // Arithmetic policies: the NTT kernels are written once against these.  Both
 // read and write canonical u64 residues; ArF64 requires q < 2^51.
 struct ArInt {
@@ -252,15 +256,31 @@ struct ArF64 {
   __device__ static uint64_t store_lazy(V x) { return bits(x); }
   __device__ static uint64_t bits(V x) { return (uint64_t)__double_as_longlong(x); }
   __device__ static V unbits(uint64_t b) { return __longlong_as_double((long long)b); }
+  // (one uniform branch per call on lz: passed into the stages, it is
+  // if-converted -- both reductions computed, one selected -- see ArF64Row)
   template <int LE>
   __device__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
   {
+#if F64_LZ_CALL
+    if (lz)
+      fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv, true);
+    else
+      fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv, false);
+#else
     fwd_stages_f<LE>(x, tw, bb, log_thi, q, qinv, lz);
+#endif
   }
   template <int LE>
   __device__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
+#if F64_LZ_CALL
+    if (lz)
+      inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv, true);
+    else
+      inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv, false);
+#else
     inv_stages_f<LE>(x, itw, bb, log_tlo, q, qinv, lz);
+#endif
   }
   __device__ uint64_t mulc(V x, uint64_t w, uint64_t) const
   {
@@ -432,7 +452,8 @@ struct ArF64Row : ArF64 {
   // LZC: the lazy-reduction choice -- 0 / 1 at compile time, -1 one uniform
   // branch per call (fwd / inv below), -2 per element at run time (which the
   // compiler if-converts: both reductions computed, one selected, so every
-  // modulus pays the wide one; fewer registers than -1 in some kernels)
+  // modulus pays the wide one; fewer registers than -1 in some kernels);
+  // -3 / -4: per call forward and per element inverse / the reverse
   __device__ __forceinline__ double2 twf(const uint64_t *tab, uint64_t e) const
   {
     if constexpr (W8) {
@@ -448,8 +469,9 @@ struct ArF64Row : ArF64 {
   template <int LE>
   __device__ __forceinline__ void fwd(V (&x)[1 << LE], uint64_t bb, int log_thi) const
   {
-    if constexpr (LZC != -1)
-      fwd_p<LE, LZC>(x, bb, log_thi);
+    constexpr int FM = LZC == -3 ? -1 : LZC == -4 ? -2 : LZC;
+    if constexpr (FM != -1)
+      fwd_p<LE, FM>(x, bb, log_thi);
     else if (lz)
       fwd_p<LE, 1>(x, bb, log_thi);
     else
@@ -458,10 +480,11 @@ struct ArF64Row : ArF64 {
   template <int LE>
   __device__ __forceinline__ void inv(V (&x)[1 << LE], uint64_t bb, int log_tlo) const
   {
+    constexpr int IM = LZC == -3 ? -2 : LZC == -4 ? -1 : LZC;
     if (GINV || (!W8 && !itl))  // (uniform) no staged inverse table: the global one
       ArF64::inv<LE>(x, bb, log_tlo);
-    else if constexpr (LZC != -1)
-      inv_p<LE, LZC>(x, bb, log_tlo);
+    else if constexpr (IM != -1)
+      inv_p<LE, IM>(x, bb, log_tlo);
     else if (lz)
       inv_p<LE, 1>(x, bb, log_tlo);
     else
@@ -1185,6 +1208,15 @@ void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, c
 // cols_mixed.hip: the same for prime sets mixing FP64 and wider integer
 // moduli (GPQHE_COLSM; replaces ks_cols4_kernel<., 8, true, false> and
 // dn_cols_kernel<., 8, ., false, true>)
+// GPQHE_COLSM_MB: more targets than one block's 8 (config 5: 12) as target
+// batches, each re-running the digit's column INTT, instead of a separate
+// column pass of y; GPQHE_COLSM_DN8: dn_colsm at T = 256 too
+#ifndef GPQHE_COLSM_MB
+#define GPQHE_COLSM_MB 0
+#endif
+#ifndef GPQHE_COLSM_DN8
+#define GPQHE_COLSM_DN8 0
+#endif
 #ifndef GPQHE_COLSM
 #define GPQHE_COLSM 1
 #endif
