@@ -2308,12 +2308,14 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
 static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)
 {
   check_ctx();
-  // groups of ~192 MiB: a group's column-pass output is still in the 256 MB
+  // groups of ~224 MiB: a group's column-pass output is still in the 256 MB
   // Infinity Cache when its row pass reads it (config 2, 1024 polys x 8 limbs
   // at N=2^16: roundtrip 8.41 -> 7.84 ms; 32-64 MiB groups lose more to
-  // launch gaps than they gain)
+  // launch gaps than they gain).  Sweep (scripts/gpu_ntt_group.sh, same box,
+  // ms): 96 7.46-7.56, 160 7.20-7.26, 192 6.84-6.92, 224 6.62-6.82, 240
+  // 6.76-6.77, 256 6.72-7.04, 320 7.24, 512 7.42, whole batch 7.31-7.34.
   // (GPQHE_NTT_GROUP_MIB: the group size for sweeps)
-  static const size_t group_mib = env_u("GPQHE_NTT_GROUP_MIB", 192);
+  static const size_t group_mib = env_u("GPQHE_NTT_GROUP_MIB", 224);
   const size_t per = std::max<size_t>(1, std::min<size_t>(65535 / nlimbs, (group_mib << 20) /
                                                                               ((size_t)nlimbs * G.n * 8)));
   for (size_t p0 = 0; p0 < npolys; p0 += per) {
