@@ -4,6 +4,7 @@
 #include "ntt_device.h"
 
 #include <algorithm>
+#include <numeric>
 
 // ksq_kernel<keep> on FP64 prime sets: loads issued one phase ahead (below);
 // -DKSQ_KEEP_PF=0 builds the load-before-use form (same-box A/B)
@@ -29,6 +30,10 @@
 // selected -- so every slot paid the non-lazy cost
 #ifndef KSQ_LZ_CT
 #define KSQ_LZ_CT 0
+#endif
+// grids of whole waves of workgroups (ksq_launch); 0 off
+#ifndef KSQ_FILL
+#define KSQ_FILL 0
 #endif
 // the dropped slots' run-time lazy choice (ArF64Row LZC: -2 per element)
 #ifndef KSQ_DROP_LZM
@@ -434,6 +439,14 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
   unsigned members = std::max(1u, (count + per - 1) / per);
   while (members < count && (size_t)groups * members < 2 * 256)
     members++;
+  if (KSQ_FILL && count >= 64) {
+    // one workgroup per CU (the key tile's LDS): a grid of whole waves of
+    // 256 workgroups leaves no partly idle last wave.  1: fewer, longer pair
+    // ranges; 2: more, shorter ones
+    const unsigned step = 256 / std::gcd(groups, 256u);
+    const unsigned lo = std::max(step, members / step * step), hi = (members + step - 1) / step * step;
+    members = std::min(count, KSQ_FILL == 1 ? lo : hi);
+  }
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const size_t t1_stride = (size_t)NDIG * nm * n;
   auto kern = keep_stage ? ksq_kernel<LOGN2, NDIG, QN, AR, true, LTW> : ksq_kernel<LOGN2, NDIG, QN, AR, false, DROP_LTW>;
