@@ -31,9 +31,12 @@
 #ifndef KSQ_LZ_CT
 #define KSQ_LZ_CT 0
 #endif
-// grids of whole waves of workgroups (ksq_launch); 0 off
+// grids of whole waves of workgroups (ksq_launch): same box, single stream,
+// keep 1855 -> 1824-1848, drop 1159 -> 1105-1116 us per chunk; two streams
+// (whose kernels fill each other's tails) unchanged.  0 off, 2 shorter ranges
+// (slower)
 #ifndef KSQ_FILL
-#define KSQ_FILL 0
+#define KSQ_FILL 1
 #endif
 // the dropped slots' run-time lazy choice (ArF64Row LZC: -2 per element)
 #ifndef KSQ_DROP_LZM
