@@ -447,8 +447,10 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
     // 256 workgroups leaves no partly idle last wave.  1: fewer, longer pair
     // ranges; 2: more, shorter ones
     const unsigned step = 256 / std::gcd(groups, 256u);
+    if (step <= 16) {  // (else the rounding would cut the ranges to a few pairs)
     const unsigned lo = std::max(step, members / step * step), hi = (members + step - 1) / step * step;
     members = std::min(count, KSQ_FILL == 1 ? lo : hi);
+    }
   }
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const size_t t1_stride = (size_t)NDIG * nm * n;
