@@ -38,9 +38,12 @@
 #ifndef KSQ_FILL
 #define KSQ_FILL 1
 #endif
-// the dropped slots' run-time lazy choice (ArF64Row LZC: -2 per element)
+// the dropped slots' run-time lazy choice (ArF64Row LZC): -4 per element in
+// the forward passes, one branch per call in the inverse ones (52 B/lane of
+// spills; drop 1114 -> 1107 us per chunk, same box); -2 per element in both
+// (44 B); -1 per call in both spilled 92 B (1196 -> 1258 us)
 #ifndef KSQ_DROP_LZM
-#define KSQ_DROP_LZM -2
+#define KSQ_DROP_LZM -4
 #endif
 // mixed prime sets: each arithmetic class's slot runs on its own kernel
 #ifndef KSQ_SPLIT_AR
@@ -79,6 +82,30 @@
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
 // ===========================================================================
+// streamed operand loads (T1, inputs, conv: each word read once per kernel)
+// as non-temporal loads: measured slower (keep 1853 -> 2140 us per chunk: a
+// thread's two input halves share cache lines), off
+#ifndef KSQ_NT_LD
+#define KSQ_NT_LD 0
+#endif
+typedef uint64_t ksq_u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint64_t ksq_ld(const uint64_t *p)
+{
+  if constexpr (KSQ_NT_LD)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+__device__ __forceinline__ ulonglong2 ksq_ld2(const ulonglong2 *p)
+{
+  if constexpr (KSQ_NT_LD) {
+    const ksq_u64x2 v = __builtin_nontemporal_load((const ksq_u64x2 *)p);
+    return make_ulonglong2(v.x, v.y);
+  } else {
+    return *p;
+  }
+}
+
 // the policy with its lazy-reduction choice fixed (LZ 0 / 1; -1 as it is)
 template <int LZ>
 __device__ __forceinline__ ArF64 with_lz(ArF64 a)
@@ -150,7 +177,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     const uint64_t *s = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      x[k] = s[(row << LOGN2) + l + T::TA * k];
+      x[k] = ksq_ld(&s[(row << LOGN2) + l + T::TA * k]);
   };
   unsigned p = pb0 + qi;
   uint64_t xn[NX > 0 ? NX : 1][8];
@@ -217,7 +244,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int a = 0; a < 4; a++) {
           const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4 * h);
-          const ulonglong2 w0 = v2[0], w1 = v2[1];
+          const ulonglong2 w0 = ksq_ld2(&v2[0]), w1 = ksq_ld2(&v2[1]);
           inw[a][0] = w0.x;
           inw[a][1] = w0.y;
           inw[a][2] = w1.x;
@@ -250,7 +277,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           const uint64_t *cv = conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff;
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            w[k] = cv[(row << LOGN2) + l + T::TA * k];
+            w[k] = ksq_ld(&cv[(row << LOGN2) + l + T::TA * k]);
         }
       };
       if ((EARLY || KPL) && jo < NDIG)
@@ -305,7 +332,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
                 for (int a = 0; a < 4; a++) {
                   const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4);
-                  const ulonglong2 w0 = v2[0], w1 = v2[1];
+                  const ulonglong2 w0 = ksq_ld2(&v2[0]), w1 = ksq_ld2(&v2[1]);
                   inw2[a][0] = w0.x;
                   inw2[a][1] = w0.y;
                   inw2[a][2] = w1.x;
@@ -379,7 +406,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           } else {
 #pragma unroll
             for (int k = 0; k < 8; k++)
-              r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
+              r[k] = A::load_lazy(EARLY ? cvw[half][k] : ksq_ld(&cv[(row << LOGN2) + l + T::TA * k]));  // conv (lazy)
           }
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
@@ -421,8 +448,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
     }
     };
     // (run-time choice: one branch per transform call for the kept slots,
-    // 1811 vs 1831 us per chunk; per element for the dropped ones, whose
-    // registers the branch form spills: 1196 vs 1258)
+    // 1811 vs 1831 us per chunk; KSQ_DROP_LZM for the dropped ones, whose
+    // registers the all-branch form spills)
     pairs(std::integral_constant<int, !F ? -1 : AR < 3 ? (KEEP ? -1 : KSQ_DROP_LZM) : AR == 3 ? 1 : 0>{});
   });
 }
