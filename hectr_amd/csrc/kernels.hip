@@ -3736,6 +3736,9 @@ bool k_mul_split_ok(unsigned lvl)
 }
 
 hipEvent_t g_split_after_d2 = nullptr;
+#ifndef GPQHE_SPLIT_SHIFT
+#define GPQHE_SPLIT_SHIFT 1
+#endif
 
 template <int LOGT1, int LOGN2>
 static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
@@ -3761,10 +3764,16 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   uint64_t *conv = accd + (size_t)2 * count * nd * n;
   const D01Src d01{a, b, in_stride, in_pstride};
   const bool allf = up.f64 && dn.f64;
+  // (two-stream sub-chunks, api.cpp: the second starts when this one has run
+  // GPQHE_SPLIT_SHIFT stages -- 1: d2_rows, 2: + ks_cols)
+  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 0)
+    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
   d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc);
-  if (g_split_after_d2)  // (experiment: two-stream pipelining)
+  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 1)
     HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
   ks_cols_stage<LOGT1>(y, T1, count, lvl, invc);
+  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 2)
+    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
   {
     // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per
     // workgroup; writes the inverse row pass of the nd dropped slots
