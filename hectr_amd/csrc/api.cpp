@@ -2318,7 +2318,12 @@ static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inver
   static const size_t group_mib = env_u("GPQHE_NTT_GROUP_MIB", 224);
   const size_t per = std::max<size_t>(1, std::min<size_t>(65535 / nlimbs, (group_mib << 20) /
                                                                               ((size_t)nlimbs * G.n * 8)));
-  for (size_t p0 = 0; p0 < npolys; p0 += per) {
+  // the inverse walks the groups from the last one (GPQHE_NTT_REV): after a
+  // forward batch, its last group's output is what the Infinity Cache holds
+  static const bool rev = env_u("GPQHE_NTT_REV", 1) != 0;
+  const size_t ngroups = (npolys + per - 1) / per;
+  for (size_t i = 0; i < ngroups; i++) {
+    const size_t g = inverse && rev ? ngroups - 1 - i : i, p0 = g * per;
     const unsigned cnt = (unsigned)std::min(per, npolys - p0);
     k_ntt(qlimbs(data + p0 * nlimbs * G.n, nlimbs, cnt, (size_t)nlimbs * G.n), inverse);
   }
