@@ -2305,6 +2305,65 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   }
 }
 
+static bool gemv_batch_fast(uint64_t *, const double *, const uint64_t *, size_t, unsigned, const he_evk_t *)
+{
+  return false;
+}
+
+static bool rot_batch_fast(uint64_t *, const uint64_t *, size_t, unsigned, unsigned, const he_evk_t *)
+{
+  return false;
+}
+
+// A ciphertext of a batch as an object view (no payload of its own).
+static he_ct_t ct_view(const uint64_t *base, unsigned nlimbs)
+{
+  he_ct_t c{};
+  c.data = (uint64_t *)base;
+  c.nlimbs = c.cap = nlimbs;
+  c.npoly = 2;
+  c.scale = 1.0;
+  return c;
+}
+
+extern "C" void he_gemv_batch(uint64_t *y, const gpqhe_complex_t M[], const uint64_t *x, size_t count,
+                              unsigned int nlimbs, const he_evk_t rk[])
+{
+  check_ctx();
+  const unsigned lvl = nlimbs;
+  if (lvl < 2 || lvl > G.L)
+    gpqhe_die("he_gemv_batch: bad level %u", lvl);
+  const size_t n = G.n, in_words = 2 * (size_t)lvl * n, out_words = 2 * (size_t)(lvl - 1) * n;
+  if (count && y < x + count * in_words && x < y + count * out_words)
+    gpqhe_die("he_gemv_batch: output overlaps the input");
+  if (gemv_batch_fast(y, (const double *)M, x, count, lvl, rk))
+    return;
+  // one ciphertext at a time on the per-call path (its diagonals cached
+  // after the first)
+  for (size_t i = 0; i < count; i++) {
+    he_ct_t cx = ct_view(x + i * in_words, lvl), cy = ct_view(y + i * out_words, lvl - 1);
+    gemv_now(&cy, (const double *)M, &cx, rk, lvl);
+  }
+}
+
+extern "C" void he_rot_batch(uint64_t *out, const uint64_t *x, size_t count, unsigned int nlimbs, unsigned int rot,
+                             const he_evk_t rk[])
+{
+  check_ctx();
+  const unsigned lvl = nlimbs;
+  if (lvl < 1 || lvl > G.L)
+    gpqhe_die("he_rot_batch: bad level %u", lvl);
+  const size_t words = 2 * (size_t)lvl * G.n;
+  if (count && out < x + count * words && x < out + count * words)
+    gpqhe_die("he_rot_batch: output overlaps the input");
+  if (rot % G.slots && rot_batch_fast(out, x, count, lvl, rot % G.slots, rk))
+    return;
+  for (size_t i = 0; i < count; i++) {
+    he_ct_t cx = ct_view(x + i * words, lvl), co = ct_view(out + i * words, lvl);
+    he_rot(&co, &cx, rot, rk);
+  }
+}
+
 static void ntt_batch(uint64_t *data, size_t npolys, unsigned nlimbs, bool inverse)
 {
   check_ctx();

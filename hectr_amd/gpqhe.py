@@ -128,6 +128,8 @@ SIGNATURES = {
     "he_mul_pt": (None, [OBJ, OBJ, OBJ]),
     "he_add_pt": (None, [OBJ, OBJ, OBJ]),
     "he_mul_rescale_batch": (None, [VP, VP, VP, C.c_size_t, C.c_uint, OBJ]),
+    "he_gemv_batch": (None, [VP, VP, VP, C.c_size_t, C.c_uint, OBJ]),
+    "he_rot_batch": (None, [VP, VP, C.c_size_t, C.c_uint, C.c_uint, OBJ]),
     "poly_ntt_batch": (None, [VP, C.c_size_t, C.c_uint]),
     "poly_intt_batch": (None, [VP, C.c_size_t, C.c_uint]),
     "poly_fill_uniform": (None, [VP, C.c_size_t, C.c_uint, C.c_uint64]),

@@ -203,6 +203,17 @@ void he_add_pt(he_ct_t *out, const he_ct_t *a, const he_pt_t *pt);  /* [ext] */
 /* ------------------------------------------------------------------------ */
 void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uint64_t *b,
                           size_t count, unsigned int nlimbs, const he_evk_t *rlk);
+/* he_gemv over `count` independent ciphertexts that share M and the rotation
+ * keys (HECTR's encrypted matrix-vector step, reference src/hempc.c:257,259,
+ * with its rotation keys from src/ctr.c:521,526-532, batched across a
+ * ciphertext batch): x [count][2][nlimbs][n] -> y [count][2][nlimbs-1][n],
+ * each y_i = M x_i with the residues he_gemv gives it.  y must not overlap x. */
+void he_gemv_batch(uint64_t *y, const gpqhe_complex_t M[], const uint64_t *x,
+                   size_t count, unsigned int nlimbs, const he_evk_t rk[]);
+/* he_rot of `count` ciphertexts by the same rotation:
+ * x [count][2][nlimbs][n] -> out [count][2][nlimbs][n]; no overlap. */
+void he_rot_batch(uint64_t *out, const uint64_t *x, size_t count,
+                  unsigned int nlimbs, unsigned int rot, const he_evk_t rk[]);
 /* npolys contiguous polynomials [npolys][nlimbs][n], limb i mod q_i. */
 void poly_ntt_batch(uint64_t *data, size_t npolys, unsigned int nlimbs);
 void poly_intt_batch(uint64_t *data, size_t npolys, unsigned int nlimbs);

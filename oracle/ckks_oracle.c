@@ -1577,29 +1577,21 @@ void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const he_evk_t rk
 /* y = M x, diagonal method (Halevi-Shoup) with hoisted ModUp and a single
  * ModDown-and-rescale by P * q_{lvl-1} at the end.  Diagonal d is encoded at
  * scale q_{lvl-1} over the QP basis so that y keeps x's scale exactly. */
-void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
+/* The non-zero diagonals of M (diagonal d: M[i][(i + d) mod s]), encoded at
+ * scale q_{lvl-1} over basis_qp(lvl) in NTT form: *pt [cnt][nm][n], rot[e]
+ * the rotation of the e-th one (ascending).  Returns cnt. */
+static unsigned gemv_diags(uint64_t **pt, unsigned *rot, const gpqhe_complex_t M[], unsigned lvl)
 {
-  check_ctx();
-  const unsigned lvl = x->nlimbs, s = C.slots;
-  if (lvl < 2)
-    die("he_gemv: input at the lowest level");
+  const unsigned s = C.slots;
   const size_t n = C.n;
   unsigned mods[MAXMOD];
   const unsigned nm = basis_qp(lvl, mods);
   const double complex *Mz = (const double complex *)M;
-  uint64_t *c1c = xmalloc((size_t)lvl * n * 8);
-  for (unsigned m = 0; m < lvl; m++) {
-    memcpy(c1c + (size_t)m * n, LIMB(x, 1, m), n * 8);
-    intt_limb(c1c + (size_t)m * n, m);
-  }
-  const unsigned ndig = (lvl + C.alpha - 1) / C.alpha;
-  uint64_t *D = xmalloc((size_t)ndig * nm * n * 8);
-  modup(D, LIMB(x, 1, 0), c1c, lvl);
-  uint64_t *acc0 = xcalloc((size_t)nm * n * 8), *acc1 = xcalloc((size_t)nm * n * 8);
-  uint64_t *ptl = xmalloc((size_t)nm * n * 8);
   int64_t *coef = xmalloc(n * sizeof(int64_t));
   double complex *diag = xmalloc((size_t)s * sizeof(double complex));
+  uint64_t *all = xmalloc((size_t)s * nm * n * 8);
   const double qtop = (double)C.q[lvl - 1];
+  unsigned cnt = 0;
   for (unsigned d = 0; d < s; d++) {
     int nz = 0;
     for (unsigned i = 0; i < s; i++) {
@@ -1609,10 +1601,41 @@ void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_e
     if (!nz)
       continue;
     encode_coeffs(coef, diag, s, qtop);
+    uint64_t *ptl = all + (size_t)cnt * nm * n;
     for (unsigned t = 0; t < nm; t++) {
       lift_i64(ptl + (size_t)t * n, coef, mods[t]);
       ntt_limb(ptl + (size_t)t * n, mods[t]);
     }
+    rot[cnt++] = d;
+  }
+  free(diag);
+  free(coef);
+  *pt = all;
+  return cnt;
+}
+
+/* y = sum over the encoded diagonals e of pt_e * rot_{rot[e]}(x): one hoisted
+ * ModUp of x, the inner products in the extended basis, one ModDown by
+ * P q_{lvl-1}. */
+static void gemv_apply(he_ct_t *y, const he_ct_t *x, const he_evk_t rk[], const uint64_t *pts,
+                       const unsigned *rot, unsigned cnt)
+{
+  const unsigned lvl = x->nlimbs;
+  const size_t n = C.n;
+  unsigned mods[MAXMOD];
+  const unsigned nm = basis_qp(lvl, mods);
+  uint64_t *c1c = xmalloc((size_t)lvl * n * 8);
+  for (unsigned m = 0; m < lvl; m++) {
+    memcpy(c1c + (size_t)m * n, LIMB(x, 1, m), n * 8);
+    intt_limb(c1c + (size_t)m * n, m);
+  }
+  const unsigned ndig = (lvl + C.alpha - 1) / C.alpha;
+  uint64_t *D = xmalloc((size_t)ndig * nm * n * 8);
+  modup(D, LIMB(x, 1, 0), c1c, lvl);
+  uint64_t *acc0 = xcalloc((size_t)nm * n * 8), *acc1 = xcalloc((size_t)nm * n * 8);
+  for (unsigned e = 0; e < cnt; e++) {
+    const unsigned d = rot[e];
+    const uint64_t *ptl = pts + (size_t)e * nm * n;
     if (d == 0) {
       /* acc += pt * P * (c0, c1) on the q limbs (P limbs: 0) */
       for (unsigned t = 0; t < lvl; t++) {
@@ -1634,18 +1657,73 @@ void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_e
   const double scale = x->scale;
   ks_finish(y, acc0, acc1, lvl, 1);
   y->scale = scale;
-  free(diag);
-  free(coef);
-  free(ptl);
   free(acc0);
   free(acc1);
   free(D);
   free(c1c);
 }
 
+void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x, const he_evk_t rk[])
+{
+  check_ctx();
+  const unsigned lvl = x->nlimbs;
+  if (lvl < 2)
+    die("he_gemv: input at the lowest level");
+  uint64_t *pts;
+  unsigned *rot = xmalloc((size_t)C.slots * sizeof(unsigned));
+  const unsigned cnt = gemv_diags(&pts, rot, M, lvl);
+  gemv_apply(y, x, rk, pts, rot, cnt);
+  free(pts);
+  free(rot);
+}
+
 /* ======================================================================== */
 /* Batched entry points                                                      */
 /* ======================================================================== */
+static he_ct_t ct_view(const uint64_t *base, unsigned nlimbs)
+{
+  he_ct_t c = {0};
+  c.data = (uint64_t *)base;
+  c.nlimbs = c.cap = nlimbs;
+  c.npoly = 2;
+  c.scale = 1.0;
+  return c;
+}
+
+/* Independent ciphertexts, one thread each (the per-ciphertext kernels'
+ * own parallel loops stay serial inside); the diagonals are encoded once. */
+void he_gemv_batch(uint64_t *y, const gpqhe_complex_t M[], const uint64_t *x, size_t count, unsigned int nlimbs,
+                   const he_evk_t rk[])
+{
+  check_ctx();
+  if (nlimbs < 2 || nlimbs > C.L)
+    die("he_gemv_batch: bad level %u", nlimbs);
+  uint64_t *pts;
+  unsigned *rot = xmalloc((size_t)C.slots * sizeof(unsigned));
+  const unsigned cnt = gemv_diags(&pts, rot, M, nlimbs);
+  const size_t in_words = (size_t)2 * nlimbs * C.n, out_words = (size_t)2 * (nlimbs - 1) * C.n;
+#pragma omp parallel for schedule(dynamic)
+  for (size_t i = 0; i < count; i++) {
+    he_ct_t cx = ct_view(x + i * in_words, nlimbs), cy = ct_view(y + i * out_words, nlimbs - 1);
+    gemv_apply(&cy, &cx, rk, pts, rot, cnt);
+  }
+  free(pts);
+  free(rot);
+}
+
+void he_rot_batch(uint64_t *out, const uint64_t *x, size_t count, unsigned int nlimbs, unsigned int rot,
+                  const he_evk_t rk[])
+{
+  check_ctx();
+  if (nlimbs < 1 || nlimbs > C.L)
+    die("he_rot_batch: bad level %u", nlimbs);
+  const size_t words = (size_t)2 * nlimbs * C.n;
+#pragma omp parallel for schedule(dynamic)
+  for (size_t i = 0; i < count; i++) {
+    he_ct_t cx = ct_view(x + i * words, nlimbs), co = ct_view(out + i * words, nlimbs);
+    he_rot(&co, &cx, rot, rk);
+  }
+}
 void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uint64_t *b,
                           size_t count, unsigned int nlimbs, const he_evk_t *rlk)
 {
