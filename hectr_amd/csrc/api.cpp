@@ -88,6 +88,24 @@ struct Ws {
   Ws &operator=(const Ws &) = delete;
 };
 
+// Folded gemv / rotation keys (see gemv_fold below).
+static uint64_t g_key_gen = 1;
+struct FoldEntry {
+  std::vector<double> M;  // the matrix (he_gemv); empty for a rotation
+  unsigned s, lvl, rot;
+  uint64_t gen;
+  const he_evk_t *rk;
+  std::vector<unsigned> d;  // rotation of each folded diagonal
+  double *K;
+  size_t bytes;
+};
+static std::vector<FoldEntry> g_folds;
+
+static void fold_cache_clear();
+static bool gemv_win_on(unsigned lvl);
+static const FoldEntry &gemv_fold(const double *Md, unsigned lvl, const he_evk_t rk[]);
+static const FoldEntry &rot_fold(unsigned r, unsigned lvl, const he_evk_t rk[]);
+
 // Pinned staging ring for small host->device uploads (encode).
 struct Stage {
   void *host = nullptr;
@@ -728,6 +746,8 @@ extern "C" void hectx_exit(void)
   check_ctx();
   HIP_CHECK(hipStreamSynchronize(G.stream));
   gemv_cache_clear();
+  fold_cache_clear();
+  g_key_gen++;
   tables_free();
   g_spec = SpecNoise{};  // its blocks go with the pool
   g_spec_next_k = 0;
@@ -825,6 +845,7 @@ static void evk_make_mont(he_evk_t *evk)
 
 extern "C" void he_free_evk(he_evk_t *evk)
 {
+  g_key_gen++;
   if (evk->reserved && G.init)
     pool_free((void *)(uintptr_t)evk->reserved);
   obj_free(evk);
@@ -867,8 +888,10 @@ extern "C" void he_import(void *vo, const uint64_t *host, unsigned int nlimbs, d
   o->nlimbs = nlimbs;
   o->scale = scale;
   o->flags = flags;
-  if (o->dnum && o->npoly == 2 * o->dnum && o->cap == G.nmod)
+  if (o->dnum && o->npoly == 2 * o->dnum && o->cap == G.nmod) {
+    g_key_gen++;
     evk_make_mont((he_evk_t *)o);  // key objects keep their Montgomery shadow in sync
+  }
 }
 
 extern "C" void he_evk_meta(const he_evk_t *evk, uint32_t *galois, uint32_t *dnum)
@@ -897,6 +920,7 @@ extern "C" void he_keypair(he_pk_t *pk, poly_mpi_t *sk)
 
 static void gen_evk(he_evk_t *evk, const uint64_t *sprime, const poly_mpi_t *sk, uint32_t galois)
 {
+  g_key_gen++;
   if (evk->data)
     he_free_evk(evk);
   obj_alloc(evk, 2 * G.dnum, G.nmod);
@@ -1790,6 +1814,15 @@ extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const 
   const size_t n = G.n;
   const uint64_t g = galois_of_rot(rot);
   const he_evk_t *k = find_rot_key(rk, rot, g);
+  if (gemv_win_on(lvl)) {  // (reads every input word before the ModDown writes out: in place is fine)
+    const FoldEntry &f = rot_fold(rot, lvl, rk);
+    const double scale = in->scale;
+    k_gemv_batch_ex(out->data, 0, pstride(out), in->data, 0, pstride(in), 1, lvl, f.K, f.d.data(), 1, 0);
+    out->nlimbs = lvl;
+    out->scale = scale;
+    out->flags = 0;
+    return;
+  }
   Ws D((size_t)ndig * nm * n), acc(2 * nm * n);
   hoist_modup(D.p, in, lvl);
   k_ks_inner(acc.p, D.p, 1, 0, 0, k->data, lvl, g, limb(in, 0, 0), nullptr, 0, nullptr, false);
@@ -2065,6 +2098,19 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   if (lvl < 2)
     gpqhe_die("he_gemv: input at the lowest level");
   const double *Md = (const double *)M;
+  if (gemv_win_on(lvl)) {  // n >= 2^13, FP64 prime sets: the windowed batch path, one ciphertext
+    if (lazy)
+      flush_ew();
+    check_ctx();
+    prov_forget(y->data, pstride(y));
+    const FoldEntry &f = gemv_fold(Md, lvl, rk);
+    const double scale = x->scale;
+    k_gemv_batch_ex(y->data, 0, pstride(y), x->data, 0, pstride(x), 1, lvl, f.K, f.d.data(), (unsigned)f.d.size(), 1);
+    y->nlimbs = lvl - 1;
+    y->scale = scale;
+    y->flags = 0;
+    return;
+  }
   // queue behind the pending gemv only when the two are independent, at one
   // level, with one output layout, and no diagonal encode can clear the
   // cache the pending one refers to
@@ -2305,14 +2351,117 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   }
 }
 
-static bool gemv_batch_fast(uint64_t *, const double *, const uint64_t *, size_t, unsigned, const he_evk_t *)
+// ---------------------------------------------------------------------------
+// he_gemv / he_rot on the windowed FP64 path (gemv_win.hip) for n >= 2^13 and
+// prime sets below 2^51.  The rotation keys are folded with their diagonals
+// once and cached: HECTR passes the same gain matrices every control step
+// (src/hempc.c:232-238), the bench the same matrix every step.  Any change of
+// a key (generation, import, free) drops every folded set (g_key_gen).
+// ---------------------------------------------------------------------------
+static void fold_cache_clear()
 {
-  return false;
+  for (FoldEntry &f : g_folds)
+    pool_free(f.K);
+  g_folds.clear();
 }
 
-static bool rot_batch_fast(uint64_t *, const uint64_t *, size_t, unsigned, unsigned, const he_evk_t *)
+static const FoldEntry &fold_insert(FoldEntry &&f)
 {
-  return false;
+  // a few sets (a 16-slot gemv at N=2^16, L=8 folds to 480 MB)
+  static const size_t cap = (size_t)env_u("GPQHE_FOLD_MIB", 16384) << 20;
+  size_t total = f.bytes;
+  for (const FoldEntry &e : g_folds)
+    total += e.bytes;
+  while (!g_folds.empty() && (g_folds.size() >= 8 || total > cap)) {
+    total -= g_folds.front().bytes;
+    pool_free(g_folds.front().K);
+    g_folds.erase(g_folds.begin());
+  }
+  g_folds.push_back(std::move(f));
+  return g_folds.back();
+}
+
+static bool gemv_win_on(unsigned lvl)
+{
+  static const bool on = env_u("GPQHE_GEMV_WIN", 1) != 0;
+  return on && k_gemv_win_ok(lvl);
+}
+
+// The non-zero diagonals of M, encoded at scale q_{lvl-1} over basis_qp(lvl),
+// folded with their rotation keys.
+static const FoldEntry &gemv_fold(const double *Md, unsigned lvl, const he_evk_t rk[])
+{
+  const unsigned s = G.slots;
+  const size_t mwords = 2 * (size_t)s * s;
+  for (const FoldEntry &f : g_folds)
+    if (!f.M.empty() && f.s == s && f.lvl == lvl && f.gen == g_key_gen && f.rk == rk &&
+        !memcmp(f.M.data(), Md, mwords * 8))
+      return f;
+  std::vector<unsigned> ds;
+  std::vector<double> diags;
+  for (unsigned d = 0; d < s; d++) {
+    bool nz = false;
+    const size_t at = diags.size();
+    diags.resize(at + 2 * (size_t)s);
+    for (unsigned i = 0; i < s; i++) {
+      const size_t src = (size_t)i * s + (i + d) % s;
+      diags[at + 2 * i] = Md[2 * src];
+      diags[at + 2 * i + 1] = Md[2 * src + 1];
+      nz |= Md[2 * src] != 0.0 || Md[2 * src + 1] != 0.0;
+    }
+    if (nz)
+      ds.push_back(d);
+    else
+      diags.resize(at);
+  }
+  const unsigned E = (unsigned)ds.size();
+  unsigned mods[GPQHE_MAXMOD];
+  const unsigned nm = basis_qp(lvl, mods);
+  const size_t per = (size_t)nm << G.logn;
+  Ws pts((size_t)E * per);
+  std::vector<GemvDiagIn> dg(E);
+  for (unsigned e = 0; e < E; e++) {
+    encode_limbs(pts.p + e * per, diags.data() + 2 * (size_t)s * e, s, (double)G.q[lvl - 1], mods, nm);
+    dg[e].d = ds[e];
+    dg[e].pt = pts.p + e * per;
+    dg[e].evk = ds[e] ? find_rot_key(rk, ds[e], galois_of_rot(ds[e]))->data : nullptr;
+  }
+  FoldEntry f{std::vector<double>(Md, Md + mwords), s, lvl, 0, g_key_gen, rk, ds, nullptr,
+              k_gemv_fold_words(E, lvl) * 8};
+  f.K = E ? k_gemv_fold(dg.data(), E, lvl) : nullptr;
+  return fold_insert(std::move(f));
+}
+
+static const FoldEntry &rot_fold(unsigned r, unsigned lvl, const he_evk_t rk[])
+{
+  const he_evk_t *k = find_rot_key(rk, r, galois_of_rot(r));
+  for (const FoldEntry &f : g_folds)
+    if (f.M.empty() && f.rot == r && f.lvl == lvl && f.gen == g_key_gen && f.rk == rk)
+      return f;
+  const GemvDiagIn dg{r, nullptr, k->data};
+  FoldEntry f{{}, G.slots, lvl, r, g_key_gen, rk, {r}, nullptr, k_gemv_fold_words(1, lvl) * 8};
+  f.K = k_gemv_fold(&dg, 1, lvl);
+  return fold_insert(std::move(f));
+}
+
+static bool gemv_batch_fast(uint64_t *y, const double *Md, const uint64_t *x, size_t count, unsigned lvl,
+                            const he_evk_t rk[])
+{
+  if (!gemv_win_on(lvl))
+    return false;
+  const FoldEntry &f = gemv_fold(Md, lvl, rk);
+  k_gemv_batch(y, x, count, lvl, f.K, f.d.data(), (unsigned)f.d.size(), 1);
+  return true;
+}
+
+static bool rot_batch_fast(uint64_t *out, const uint64_t *x, size_t count, unsigned lvl, unsigned r,
+                           const he_evk_t rk[])
+{
+  if (!gemv_win_on(lvl))
+    return false;
+  const FoldEntry &f = rot_fold(r, lvl, rk);
+  k_gemv_batch(out, x, count, lvl, f.K, f.d.data(), 1, 0);
+  return true;
 }
 
 // A ciphertext of a batch as an object view (no payload of its own).

@@ -1,0 +1,513 @@
+// gemv_win.hip - HECTR's he_gemv (reference src/hempc.c:257-259) and he_rot
+// over a batch of independent ciphertexts at n = 2^13 .. 2^17, every modulus
+// below 2^51 (FP64 arithmetic, ntt_device.h):
+//
+//   y   = INTT(c1) x [(Q_j/q_i)^-1]                 k_ntt_ex, scale folded in
+//   Dc  = NTT(FBC(y)) on every slot outside a digit  gemv_fbc_kernel + k_ntt
+//   acc = sum_d pt_d sigma_d(KS_d(c0, c1))          gemv_win_kernel (basis QP)
+//   out = ModDown(acc) by P q_top (gemv) or P (rot) k_moddown
+//
+// The oracle's hoisted gemv (oracle/ckks_oracle.c gemv_apply): one ModUp per
+// ciphertext, the rotated inner products accumulated in the extended basis,
+// one ModDown per output.  Every step is exact modular arithmetic on canonical
+// residues, so the outputs are the oracle's bit for bit whatever the order of
+// the sums.
+//
+// The inner products.  Diagonal d reads D at the Galois permutation
+// pi_d = auto_index(., 5^d) of each output position.  Blocks of B = 2^LOGB
+// consecutive NTT positions (the top b = logn - LOGB index bits) map to
+// blocks: block e (odd, mod 2^(b+1)) feeds block 5^d e, and inside a block
+// the map is affine in the bit-reversed offset.  The blocks therefore form
+// two orbits under x5 (e = +-5^i), and output block i of an orbit reads
+// source blocks i .. i + dmax.  A workgroup owns (ciphertext, basis slot,
+// orbit) and walks its source blocks in orbit order: each source word is
+// loaded from HBM once, multiplied by every diagonal's key word, and added
+// into a ring of W output blocks of accumulators in LDS (the output position
+// of each product is another thread's, a bijection per diagonal, so one
+// barrier per step suffices); an output block leaves for HBM when its last
+// diagonal has arrived.  The keys are pre-multiplied by their diagonal
+// (pt_d x evk_d, P x pt_d) and stored in source order (gemv_fold_kernel), so
+// a thread's key words are contiguous and shared through L2 by every
+// ciphertext of the batch: the workgroups of one (slot, orbit) are placed on
+// one XCD (xcd_group).
+#include "ntt_device.h"
+#include "tables.h"
+
+#include <algorithm>
+#include <vector>
+
+__device__ __forceinline__ unsigned gw_brev(unsigned x, unsigned bits)
+{
+  return __builtin_bitreverse32(x) >> (32 - bits);
+}
+
+// NTT-domain position whose value sigma_g moves to k (kernels.hip auto_index)
+__device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsigned logn)
+{
+  const uint64_t mask = (2ull << logn) - 1;
+  const uint64_t e = ((2ull * gw_brev(k, logn) + 1) * g) & mask;
+  return gw_brev((unsigned)(e >> 1), logn);
+}
+
+// ---------------------------------------------------------------------------
+// Folded keys.  K[((t Etot + e) NW + w) n + k'] for source position k' of
+// slot t, which feeds output k = pi_d^-1(k') (NW = 2 ndig + 1):
+//   w < ndig:          [pt_d]_t[k] [b_{d,w}]_t[k]
+//   ndig <= w < 2 ndig: [pt_d]_t[k] [a_{d,w-ndig}]_t[k]
+//   w = 2 ndig:         [P pt_d]_t[k] on q slots (t < lvl), else 0
+// pt null: 1 (a rotation).  Exact integers below 2^51 as doubles.
+// grid: (n / 256, nm, diagonals of this launch)
+// ---------------------------------------------------------------------------
+struct FoldArgs {
+  static constexpr unsigned MAX = 16;
+  const uint64_t *pt[MAX], *evk[MAX];
+  uint64_t ginv[MAX];  // g_d^-1 mod 2n
+  unsigned e0;         // the launch's first diagonal in K
+};
+
+__global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, unsigned Etot, unsigned ndig,
+                                                        unsigned logn, unsigned lvl, unsigned L, unsigned nmod,
+                                                        const ModConst *mcs)
+{
+  const unsigned kp = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y, e = blockIdx.z;
+  const unsigned m = basis_mod(t, lvl, L);
+  const ModConst mc = mcs[m];
+  const uint64_t gi = fa.ginv[e];
+  const unsigned k = gi == 1 ? kp : gw_auto_index(kp, gi, logn);
+  const uint64_t *pt = fa.pt[e], *ev = fa.evk[e];
+  const uint64_t w = pt ? pt[((size_t)t << logn) + k] : 1;
+  const unsigned nw = 2 * ndig + 1;
+  double *o = K + ((((size_t)t * Etot + fa.e0 + e) * nw) << logn) + kp;
+  for (unsigned j = 0; j < ndig; j++) {
+    const uint64_t b = ev ? mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0;
+    const uint64_t a = ev ? mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0;
+    o[(size_t)j << logn] = (double)b;
+    o[(size_t)(ndig + j) << logn] = (double)a;
+  }
+  o[(size_t)(2 * ndig) << logn] = t < lvl ? (double)mul_mod(w, mc.pmod, mc) : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// ModUp conversion: Dc[p][slot] = sum_i y_i [Q_j/q_i]_t mod q_t for each digit
+// j and each basis slot t outside it (slots in that order), y the digit's
+// scaled coefficient-domain limbs.  One thread per coefficient.
+// grid: (n / 256, count)
+// ---------------------------------------------------------------------------
+struct GwMods {
+  double q[GPQHE_MAXMOD / 2], qinv[GPQHE_MAXMOD / 2];  // per basis slot of basis_qp(lvl)
+};
+
+__global__ void __launch_bounds__(256) gemv_fbc_kernel(uint64_t *Dc, size_t d_stride, const uint64_t *y,
+                                                       size_t y_stride, const double *cd, GwMods md, unsigned logn,
+                                                       unsigned lvl, unsigned nm, unsigned ndig, unsigned alpha)
+{
+  const size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t p = blockIdx.y;
+  const uint64_t *yp = y + p * y_stride + k;
+  uint64_t *dp = Dc + p * d_stride + k;
+  unsigned slot = 0;
+  for (unsigned j = 0; j < ndig; j++) {
+    const unsigned lo = j * alpha, na = min(alpha, lvl - lo);
+    double yv[8];
+#pragma unroll
+    for (unsigned i = 0; i < 8; i++)
+      yv[i] = i < na ? f64_from_u52(yp[(size_t)(lo + i) << logn]) : 0.0;
+    for (unsigned t = 0; t < nm; t++) {
+      if (t >= lo && t < lo + na)
+        continue;
+      const double q = md.q[t], qinv = md.qinv[t];
+      const double *c = cd + 2 * ((size_t)j * 8 * nm + t);  // ([Q_j/q_i]_t, that / q_t) at i stride 2 nm
+      // |term| < q (y < 2^51); two terms, then a reduction: |.| < 2.5 q
+      double s = 0;
+#pragma unroll
+      for (unsigned i = 0; i < 8; i++) {
+        if (i < na) {
+          s += f64_mulmod(yv[i], c[2 * i * nm], c[2 * i * nm + 1], q);
+          if (i & 1)
+            s = f64_red(s, q, qinv);
+        }
+      }
+      dp[(size_t)slot++ << logn] = f64_canon(s, q, qinv);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The windowed inner products (see the file comment).
+// ---------------------------------------------------------------------------
+struct GemvWin {
+  static constexpr unsigned MAXE = 16;
+  const uint64_t *x;  // ciphertext p: c0 at x + p x_stride, c1 at + x_pstride
+  size_t x_stride, x_pstride;
+  const uint64_t *Dc;  // compact ModUp digits [count][S][n]
+  size_t d_stride;
+  const double *K;  // folded keys [nm][Etot][NW][n]
+  uint64_t *acc;    // [count][2][nm][n]
+  size_t acc_stride;
+  int16_t yi[GPQHE_MAXMOD / 2][3];  // slot t, digit j: its Dc slot, -1: the own digit (c1 limb t)
+  int32_t d[MAXE];                  // rotations of this launch's diagonals, ascending
+  uint32_t hm[MAXE];                // g_e^-1 mod 2^LOGB
+  uint32_t i5[MAXE];                // g_e^-1 mod 2^(b+1): output block of a source block
+  uint64_t g[MAXE];                 // g_e mod 2n
+  GwMods md;
+  unsigned E, e0, Etot, accumulate;
+  unsigned logn, lvl, nm, count, nseg;
+};
+
+__device__ __forceinline__ double gw_center(double v, double q)
+{
+  return v > 0.5 * q ? v - q : v;
+}
+
+template <int LOGB, int W, int NDIG>
+__global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
+{
+  constexpr int B = 1 << LOGB, NW = 2 * NDIG + 1;
+  constexpr unsigned MB = B - 1;
+  __shared__ double lacc[W][2][B];
+  const unsigned logn = a.logn, bb = logn - LOGB, P = 1u << (bb - 1);
+  const uint64_t emask = (2ull << bb) - 1, nmask2 = (2ull << logn) - 1;
+  unsigned grp, p;
+  if (!xcd_group(a.count, a.nm * 2 * a.nseg, grp, p))
+    return;
+  const unsigned t = grp / (2 * a.nseg), orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
+  const unsigned o0 = seg * P / a.nseg, o1 = (seg + 1) * P / a.nseg;  // outputs owned: orbit positions [o0, o1)
+  const double q = a.md.q[t], qinv = a.md.qinv[t];
+  const bool qs = t < a.lvl;
+  const unsigned th = threadIdx.x, jh = gw_brev(th, LOGB);
+  const int E = (int)a.E, dmin = a.d[0], dmax = a.d[E - 1];
+  const bool ident = dmin == 0;
+  unsigned hj[W];  // g_e^-1 j'_hi: the output offset before the block's constant
+#pragma unroll
+  for (int e = 0; e < W; e++)
+    hj[e] = e < E ? (a.hm[e] * jh) & MB : 0;
+  const uint64_t *xb = a.x + (size_t)p * a.x_stride;
+  const uint64_t *src[NDIG];
+#pragma unroll
+  for (int j = 0; j < NDIG; j++) {
+    const int yi = a.yi[t][j];
+    src[j] = yi < 0 ? xb + a.x_pstride + ((size_t)t << logn) : a.Dc + (size_t)p * a.d_stride + ((size_t)yi << logn);
+  }
+  const uint64_t *c0s = xb + ((size_t)t << logn), *c1s = xb + a.x_pstride + ((size_t)t << logn);
+  const double *Kt = a.K + ((((size_t)t * a.Etot + a.e0) * NW) << logn);
+  uint64_t *accp = a.acc + (size_t)p * a.acc_stride + ((size_t)t << logn);
+  const size_t apoly = (size_t)a.nm << logn;
+  // source orbit positions [i0, i1): every diagonal of every owned output
+  const unsigned i0 = o0 + dmin, i1 = o1 + dmax;
+  uint64_t es = 1;  // orbit value of position i0: +-5^i0 mod 2^(b+1)
+  {
+    uint64_t bse = 5;
+    for (unsigned r = i0 % P; r; r >>= 1, bse = (bse * bse) & emask)
+      if (r & 1)
+        es = (es * bse) & emask;
+    if (orb)
+      es = (emask + 1 - es) & emask;
+  }
+  auto blk = [&](uint64_t ev) { return gw_brev((unsigned)(ev >> 1), bb); };  // block of odd e: brev((e - 1) / 2)
+  uint64_t ny[NDIG], nc0 = 0, nc1 = 0;
+  auto fetch = [&](uint64_t ev) {
+    const size_t off = ((size_t)blk(ev) << LOGB) + th;
+#pragma unroll
+    for (int j = 0; j < NDIG; j++)
+      ny[j] = src[j][off];
+    if (qs) {
+      nc0 = c0s[off];
+      if (ident)
+        nc1 = c1s[off];
+    }
+  };
+  fetch(es);
+  for (unsigned i = i0; i < i1; i++) {
+    const uint64_t ev = es;
+    es = (es * 5) & emask;
+    // centred (|.| <= q/2): every product below is < 0.875 q in magnitude
+    double y[NDIG], c0 = 0, c1 = 0;
+#pragma unroll
+    for (int j = 0; j < NDIG; j++)
+      y[j] = gw_center(f64_from_u52(ny[j]), q);
+    if (qs) {
+      c0 = gw_center(f64_from_u52(nc0), q);
+      if (ident)
+        c1 = gw_center(f64_from_u52(nc1), q);
+    }
+    if (i + 1 < i1)
+      fetch(es);
+    const size_t koff = ((size_t)blk(ev) << LOGB) + th;
+#pragma unroll
+    for (int e = 0; e < W; e++) {
+      const int o = (int)i - a.d[e];
+      if (e >= E || o < (int)o0 || o >= (int)o1)
+        continue;
+      const uint64_t eo = (ev * a.i5[e]) & emask;  // the output block's orbit value
+      const unsigned C = (unsigned)(((a.g[e] * eo) & nmask2) >> (bb + 1));
+      const unsigned addr = gw_brev((hj[e] - a.hm[e] * C) & MB, LOGB);
+      const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
+      double s0, s1;
+      if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
+        const double kP = kp[(size_t)(2 * NDIG) << logn];
+        s0 = qs ? f64_mulmod_h(c0, kP, q, qinv) : 0.0;
+        s1 = qs ? f64_mulmod_h(c1, kP, q, qinv) : 0.0;
+      } else {
+        s0 = f64_mulmod_h(y[0], kp[0], q, qinv);
+        s1 = f64_mulmod_h(y[0], kp[(size_t)NDIG << logn], q, qinv);
+#pragma unroll
+        for (int j = 1; j < NDIG; j++) {
+          if (j == 2) {  // three digits: fold before the third product (|.| stays < 3.2 q)
+            s0 = f64_red(s0, q, qinv);
+            s1 = f64_red(s1, q, qinv);
+          }
+          s0 += f64_mulmod_h(y[j], kp[(size_t)j << logn], q, qinv);
+          s1 += f64_mulmod_h(y[j], kp[(size_t)(NDIG + j) << logn], q, qinv);
+        }
+        if (qs)
+          s0 += f64_mulmod_h(c0, kp[(size_t)(2 * NDIG) << logn], q, qinv);
+      }
+      const unsigned slot = (unsigned)o & (W - 1);
+      if (e > 0) {  // (|acc| <= q/2 + |s| < 2.7 q)
+        s0 += lacc[slot][0][addr];
+        s1 += lacc[slot][1][addr];
+      }
+      if (e < E - 1) {
+        lacc[slot][0][addr] = f64_red(s0, q, qinv);
+        lacc[slot][1][addr] = f64_red(s1, q, qinv);
+      } else {
+        uint64_t *op = accp + ((size_t)blk(eo) << LOGB) + addr;
+        if (a.accumulate) {
+          s0 = f64_red(s0, q, qinv) + f64_from_u52(op[0]);
+          s1 = f64_red(s1, q, qinv) + f64_from_u52(op[apoly]);
+        }
+        op[0] = f64_canon(s0, q, qinv);
+        op[apoly] = f64_canon(s1, q, qinv);
+      }
+    }
+    __syncthreads();  // the ring slot written next step was read this step
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+static GwMods gw_mods(unsigned lvl)
+{
+  GwMods md{};
+  const unsigned nm = lvl + G.K;
+  for (unsigned t = 0; t < nm; t++) {
+    const uint64_t qq = G.q[t < lvl ? t : G.L + (t - lvl)];
+    md.q[t] = (double)qq;
+    md.qinv[t] = 1.0 / (double)qq;
+  }
+  return md;
+}
+
+bool k_gemv_win_ok(unsigned lvl)
+{
+  if (G.logn < 13 || G.logn > 17 || !G.twd || G.alpha > 8)
+    return false;
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
+  if (ndig < 1 || ndig > 3 || nm > GPQHE_MAXMOD / 2)
+    return false;
+  for (unsigned t = 0; t < nm; t++)
+    if (G.q[t < lvl ? t : G.L + (t - lvl)] >= F64_QMAX)
+      return false;
+  return true;
+}
+
+static uint64_t gw_pow(uint64_t b, uint64_t e, uint64_t mask)
+{
+  uint64_t r = 1;
+  for (; e; e >>= 1, b = (b * b) & mask)
+    if (e & 1)
+      r = (r * b) & mask;
+  return r;
+}
+
+// 5^d and 5^-d mod 2n (5 has order n / 2 there)
+static void gw_galois(unsigned d, uint64_t &g, uint64_t &gi)
+{
+  const uint64_t mask = (2ull << G.logn) - 1, ord = G.n / 2;
+  g = gw_pow(5, d % ord, mask);
+  gi = gw_pow(5, (ord - d % ord) % ord, mask);
+}
+
+size_t k_gemv_fold_words(unsigned E, unsigned lvl)
+{
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
+  return (size_t)nm * E * (2 * ndig + 1) * G.n;
+}
+
+double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
+{
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
+  double *K = (double *)pool_alloc(k_gemv_fold_words(E, lvl) * 8);
+  for (unsigned e0 = 0; e0 < E; e0 += FoldArgs::MAX) {
+    const unsigned cnt = std::min(FoldArgs::MAX, E - e0);
+    FoldArgs fa{};
+    fa.e0 = e0;
+    for (unsigned e = 0; e < cnt; e++) {
+      uint64_t g, gi;
+      gw_galois(dg[e0 + e].d, g, gi);
+      fa.pt[e] = dg[e0 + e].pt;
+      fa.evk[e] = dg[e0 + e].evk;
+      fa.ginv[e] = gi;
+    }
+    ProfScope ps(KC_GEMV_FOLD, 8.0 * G.n * cnt * nm * ((double)(2 * ndig + 1) * 2));
+    hipLaunchKernelGGL(gemv_fold_kernel, dim3(G.n / 256, nm, cnt), dim3(256), 0, G.stream, K, fa, E, ndig, G.logn, lvl,
+                       G.L, G.nmod, G.dev.mc);
+    HIP_CHECK(hipGetLastError());
+  }
+  return K;
+}
+
+template <int LOGB, int NDIG>
+static void gw_launch(unsigned span, dim3 grid, const GemvWin &a)
+{
+  if (span <= 1)
+    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 1, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
+  else if (span <= 4)
+    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 4, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
+  else if (span <= 8)
+    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 8, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
+  else
+    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 16, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
+  HIP_CHECK(hipGetLastError());
+}
+
+static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uint64_t *x, size_t x_stride,
+                       size_t x_pstride, unsigned cnt, unsigned lvl, const double *K, const unsigned *d, unsigned E,
+                       int mode)
+{
+  const UpTable &up = k_up_table(lvl);
+  const unsigned n = G.n, logn = G.logn, nm = up.nm, ndig = up.ndig, alpha = G.alpha;
+  // compact ModUp slots: digit j's targets outside it, in slot order
+  std::vector<int> yi((size_t)nm * 3, -1);
+  unsigned mods[GPQHE_MAXMOD], S = 0;
+  for (unsigned j = 0; j < ndig; j++) {
+    const unsigned lo = j * alpha, hi = std::min(lo + alpha, lvl);
+    for (unsigned t = 0; t < nm; t++) {
+      if (t >= lo && t < hi)
+        continue;
+      yi[(size_t)t * 3 + j] = (int)S;
+      mods[S++] = t < lvl ? t : G.L + (t - lvl);
+    }
+  }
+  const size_t ys = (size_t)lvl * n, ds = (size_t)S * n, as = 2 * (size_t)nm * n;
+  uint64_t *ws = (uint64_t *)pool_alloc((size_t)cnt * (ys + ds + as) * 8);
+  uint64_t *ybuf = ws, *Dc = ybuf + cnt * ys, *acc = Dc + cnt * ds;
+  // 1. y = INTT(c1) x n^-1 [(Q_j/q_i)^-1]
+  LimbSet in{}, yo{};
+  in.base = (uint64_t *)x + x_pstride;
+  in.per = lvl;
+  in.count = lvl * cnt;
+  in.stride = x_stride;
+  yo = in;
+  yo.base = ybuf;
+  yo.stride = ys;
+  for (unsigned i = 0; i < lvl; i++)
+    in.mods[i] = yo.mods[i] = (uint8_t)i;
+  k_ntt_ex(in, yo, true, up.ysc);
+  // 2. conversion to every slot outside each digit, 3. their forward NTT
+  const GwMods md = gw_mods(lvl);
+  {
+    ProfScope ps(KC_GEMV_FBC, 8.0 * n * cnt * ((double)lvl + S));
+    hipLaunchKernelGGL(gemv_fbc_kernel, dim3(n / 256, cnt), dim3(256), 0, G.stream, Dc, ds, ybuf, ys, up.cd, md, logn,
+                       lvl, nm, ndig, alpha);
+    HIP_CHECK(hipGetLastError());
+  }
+  LimbSet dl{};
+  dl.base = Dc;
+  dl.per = S;
+  dl.count = S * cnt;
+  dl.stride = ds;
+  for (unsigned i = 0; i < S; i++)
+    dl.mods[i] = (uint8_t)mods[i];
+  k_ntt(dl, false);
+  // 4. the inner products, diagonals in groups spanning at most 16 rotations
+  constexpr int LOGB = 8;
+  const unsigned P = 1u << (logn - LOGB - 1);
+  unsigned nseg = 1;
+  while (nseg < P / 8 && (size_t)cnt * nm * 2 * nseg < 2048)
+    nseg *= 2;
+  GemvWin a{};
+  a.x = x;
+  a.x_stride = x_stride;
+  a.x_pstride = x_pstride;
+  a.Dc = Dc;
+  a.d_stride = ds;
+  a.K = K;
+  a.acc = acc;
+  a.acc_stride = as;
+  for (unsigned t = 0; t < nm; t++)
+    for (unsigned j = 0; j < 3; j++)
+      a.yi[t][j] = (int16_t)yi[(size_t)t * 3 + j];
+  a.md = md;
+  a.Etot = E;
+  a.logn = logn;
+  a.lvl = lvl;
+  a.nm = nm;
+  a.count = cnt;
+  a.nseg = nseg;
+  const dim3 grid(xcd_blocks(cnt, nm * 2 * nseg));
+  bool first = true;
+  for (unsigned e0 = 0; e0 < E;) {
+    unsigned e1 = e0;
+    while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < 16)
+      e1++;
+    a.E = e1 - e0;
+    a.e0 = e0;
+    a.accumulate = first ? 0 : 1;
+    for (unsigned e = 0; e < a.E; e++) {
+      uint64_t g, gi;
+      gw_galois(d[e0 + e], g, gi);
+      a.d[e] = (int32_t)d[e0 + e];
+      a.g[e] = g;
+      a.hm[e] = (uint32_t)(gi & ((1u << LOGB) - 1));
+      a.i5[e] = (uint32_t)(gi & ((2ull << (logn - LOGB)) - 1));
+    }
+    const unsigned span = d[e1 - 1] - d[e0] + 1;
+    {
+      // reads each ciphertext's ModUp digits and c0 once, the folded keys once
+      // per slot and orbit, writes (or updates) the accumulators
+      ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + lvl + (first ? 2.0 : 4.0) * nm) +
+                                           (double)a.E * nm * (2 * ndig + 1)));
+      switch (ndig) {
+      case 1: gw_launch<LOGB, 1>(span, grid, a); break;
+      case 2: gw_launch<LOGB, 2>(span, grid, a); break;
+      default: gw_launch<LOGB, 3>(span, grid, a); break;
+      }
+    }
+    first = false;
+    e0 = e1;
+  }
+  // 5. ModDown of both accumulators of every ciphertext
+  if (!E)
+    HIP_CHECK(hipMemsetAsync(acc, 0, (size_t)cnt * as * 8, G.stream));
+  if (y_stride == 2 * y_pstride) {
+    k_moddown(y, y_pstride, acc, (size_t)nm * n, 2 * cnt, lvl, mode);
+  } else {
+    for (unsigned c = 0; c < cnt; c++)  // (one ciphertext: an object's own layout)
+      k_moddown(y + c * y_stride, y_pstride, acc + c * as, (size_t)nm * n, 2, lvl, mode);
+  }
+  pool_free(ws);
+}
+
+void k_gemv_batch_ex(uint64_t *y, size_t y_stride, size_t y_pstride, const uint64_t *x, size_t x_stride,
+                     size_t x_pstride, size_t count, unsigned lvl, const double *K, const unsigned *d, unsigned E,
+                     int mode)
+{
+  const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
+  const size_t per_ct = ((size_t)lvl + (size_t)ndig * nm + 2 * (size_t)nm) * G.n * 8;
+  const size_t budget = (size_t)8 << 30;
+  const size_t chunk = std::max<size_t>(1, std::min<size_t>(budget / per_ct, 65535 / (3 * nm)));
+  for (size_t c0 = 0; c0 < count; c0 += chunk) {
+    const unsigned cnt = (unsigned)std::min(chunk, count - c0);
+    gemv_chunk(y + c0 * y_stride, y_stride, y_pstride, x + c0 * x_stride, x_stride, x_pstride, cnt, lvl, K, d, E,
+               mode);
+  }
+}
+
+void k_gemv_batch(uint64_t *y, const uint64_t *x, size_t count, unsigned lvl, const double *K, const unsigned *d,
+                  unsigned E, int mode)
+{
+  const size_t n = G.n, keep = mode == 1 ? lvl - 1 : lvl;
+  k_gemv_batch_ex(y, 2 * keep * n, keep * n, x, 2 * (size_t)lvl * n, (size_t)lvl * n, count, lvl, K, d, E, mode);
+}

@@ -438,7 +438,50 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
                      unsigned lvl, int mode);
 bool k_prof_on();
+// Live kernel statistics (gpqhe_prof_enable): HIP events around one launch
+// on the engine stream, per kernel class (names: kernels.hip kc_names).
+enum KClass {
+  KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
+  KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
+  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP,
+  KC_MODUP_SMALL, KC_DOWN_SMALL, KC_GEMV_WIN, KC_GEMV_FBC, KC_GEMV_FOLD, KC_COUNT
+};
+struct ProfScope {
+  int cls;
+  double bytes;
+  hipEvent_t a = nullptr;
+  ProfScope(int c, double b);  // b: the launch's algorithmic bytes
+  ~ProfScope();
+  ProfScope(const ProfScope &) = delete;
+  ProfScope &operator=(const ProfScope &) = delete;
+};
 void k_to_mont(uint64_t *out, const uint64_t *in, unsigned nlimbs_total);
+struct UpTable;
+const UpTable &k_up_table(unsigned lvl);  // ModUp conversion tables of a level (kernels.hip)
+// he_gemv / he_rot over a ciphertext batch on the windowed FP64 path
+// (gemv_win.hip): every modulus of basis_qp(lvl) below 2^51, 2^13 <= n <= 2^17,
+// at most three digits
+bool k_gemv_win_ok(unsigned lvl);
+struct GemvDiagIn {
+  unsigned d;           // rotation (0: the identity)
+  const uint64_t *pt;   // encoded diagonal over basis_qp(lvl) (NTT form); null: 1
+  const uint64_t *evk;  // rotation key (null for d = 0)
+};
+// Keys folded with their diagonals, in source order: [nm][E][2 ndig + 1][n]
+// doubles (pool memory; the caller caches and frees it)
+double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl);
+size_t k_gemv_fold_words(unsigned E, unsigned lvl);
+// y [count][2][keep][n] = ModDown(sum over the folded diagonals d[e] of the
+// rotated key switch of x [count][2][lvl][n]); mode 1: by P q_{lvl-1} (he_gemv,
+// keep = lvl - 1), 0: by P (he_rot, keep = lvl)
+void k_gemv_batch(uint64_t *y, const uint64_t *x, size_t count, unsigned lvl, const double *K, const unsigned *d,
+                  unsigned E, int mode);
+// The same with explicit layouts: ciphertext c's poly p at x + c x_stride +
+// p x_pstride (y likewise); y_stride != 2 y_pstride runs one ModDown per
+// ciphertext (an object's own layout, count 1)
+void k_gemv_batch_ex(uint64_t *y, size_t y_stride, size_t y_pstride, const uint64_t *x, size_t x_stride,
+                     size_t x_pstride, size_t count, unsigned lvl, const double *K, const unsigned *d, unsigned E,
+                     int mode);
 void tables_upload();
 void tables_prewarm();
 void tables_free();

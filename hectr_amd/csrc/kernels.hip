@@ -40,11 +40,6 @@ __device__ __forceinline__ unsigned brev_dev(unsigned x, unsigned bits)
 // Live kernel statistics (gpqhe_prof_enable / gpqhe_prof_collect): HIP events
 // around each launch on the engine stream.
 // ===========================================================================
-enum KClass {
-  KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
-  KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
-  KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP, KC_MODUP_SMALL, KC_DOWN_SMALL, KC_COUNT
-};
 // kernel names as rocprofv3 reports them (template arguments <fwd>/<inv> stand
 // for the INV flag), so bench.py can match its statistics to a PMC profile
 static const char *kc_names[KC_COUNT] = {
@@ -52,7 +47,8 @@ static const char *kc_names[KC_COUNT] = {
   "down_conv_kernel", "down_combine_kernel", "ks_cols_kernel", "ks_rows_kernel", "dn_cols_kernel", "dn_rows_kernel",
   "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
-  "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>", "modup_small_kernel", "moddown_small_kernel"};
+  "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>", "modup_small_kernel", "moddown_small_kernel",
+  "gemv_win_kernel", "gemv_fbc_kernel", "gemv_fold_kernel"};
 
 struct ProfEntry {
   int cls;
@@ -75,26 +71,22 @@ static hipEvent_t prof_event()
   return e;
 }
 
-struct ProfScope {
-  int cls;
-  double bytes;
-  hipEvent_t a = nullptr;
-  ProfScope(int c, double b) : cls(c), bytes(b)
-  {
-    if (!g_prof)
-      return;
-    a = prof_event();
-    HIP_CHECK(hipEventRecord(a, G.stream));
-  }
-  ~ProfScope()
-  {
-    if (!a)
-      return;
-    hipEvent_t b = prof_event();
-    HIP_CHECK(hipEventRecord(b, G.stream));
-    g_prof_entries.push_back({cls, a, b, bytes});
-  }
-};
+ProfScope::ProfScope(int c, double b) : cls(c), bytes(b)
+{
+  if (!g_prof)
+    return;
+  a = prof_event();
+  HIP_CHECK(hipEventRecord(a, G.stream));
+}
+
+ProfScope::~ProfScope()
+{
+  if (!a)
+    return;
+  hipEvent_t b = prof_event();
+  HIP_CHECK(hipEventRecord(b, G.stream));
+  g_prof_entries.push_back({cls, a, b, bytes});
+}
 
 bool k_prof_on()
 {
@@ -1847,6 +1839,11 @@ static UpTable &up_table(unsigned lvl)
   HIP_CHECK(hipMemcpy(tab.dig, dig.data(), ndig * sizeof(UpDigit), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(tab.c, c.data(), c.size() * 8, hipMemcpyHostToDevice));
   return g_up[lvl] = tab;
+}
+
+const UpTable &k_up_table(unsigned lvl)
+{
+  return up_table(lvl);
 }
 
 

@@ -60,6 +60,18 @@ def main():
     out["gemv_batch_us_per_ct"] = t / cnt * 1e6
     t = timed(lambda: e.lib.he_rot_batch(r.data_ptr(), x.data_ptr(), cnt, L, 1, rk))
     out["rot_batch_us_per_ct"] = t / cnt * 1e6
+    # per-kernel device time of one batch of each (HIP events on the engine stream)
+    for name, fn in (("gemv_batch", lambda: e.lib.he_gemv_batch(y.data_ptr(), M.ctypes.data, x.data_ptr(), cnt, L,
+                                                                 rk)),
+                     ("rot_batch", lambda: e.lib.he_rot_batch(r.data_ptr(), x.data_ptr(), cnt, L, 1, rk))):
+        e.prof_enable(True)
+        fn()
+        e.sync()
+        st = e.prof_collect()
+        e.prof_enable(False)
+        out[name + "_kernels_us_per_ct"] = {k: round(v[1] / cnt, 2) for k, v in sorted(st.items(),
+                                                                                      key=lambda kv: -kv[1][1])}
+        out[name + "_kernels_GBs"] = {k: round(v[2] / v[1] / 1e3, 1) for k, v in st.items() if v[1] > 0}
     if args.single:
         ct = e.encrypt(rng.uniform(-1, 1, s) + 0j, pk)
         yc = e.ct()
