@@ -50,7 +50,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # one key for all ranks: the context / key replicas of every rank share these
 # seeds (the headline and 60-bit legs, and config 5)
-KEY_SEED, C5_KEY_SEED = 1000, 2000
+KEY_SEED, C5_KEY_SEED, GEMV_KEY_SEED = 1000, 2000, 3000
 # kernels of the fused he_mul_rescale_batch pipeline (n = 2^16: one launch each per chunk)
 PIPELINE = ("d2_rows_kernel", "ks_cols4_kernel", "ksq_kernel<drop>", "dn_cols_kernel", "ksq_kernel<keep>")
 
@@ -76,6 +76,9 @@ def parse(argv=None):
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT roundtrip leg (config 2)")
     ap.add_argument("--no-c5", action="store_true", help="skip the config 5 leg (n=2^17, L=12)")
     ap.add_argument("--c5-batch", type=int, default=64)
+    ap.add_argument("--no-gemv", action="store_true", help="skip the he_gemv_batch / he_rot_batch leg")
+    ap.add_argument("--gemv-batch", type=int, default=256)
+    ap.add_argument("--gemv-slots", type=int, default=16, help="slots (HECTR's own: 16) = gemv diagonals")
     ap.add_argument("--ntt-polys", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample duration per thread count")
     ap.add_argument("--streams", type=int, default=2,
@@ -197,6 +200,64 @@ class MulBatch:
 
     def close(self):
         del self.a, self.b, self.out
+        self.eng.exit()
+
+
+class GemvBatch:
+    """he_gemv_batch / he_rot_batch: HECTR's encrypted matrix-vector step
+    (reference src/hempc.c:257-259, `slots` rotation keys from src/ctr.c:521,
+    526-532) over a batch of independent ciphertexts sharing the matrix and the
+    keys (north_star: the hempc ciphertext batch).  Ciphertext g of the global
+    batch comes from seed + g alone (any sharding sees the same inputs); M is a
+    dense random complex slots x slots matrix (every diagonal non-zero)."""
+
+    def __init__(self, stream, logn, L, dnum, q0_bits, p_bits, nspecial, slots, batch, first, seed):
+        import numpy as np
+        import torch
+        from hectr_amd.gpqhe import Engine
+        self.K = nspecial or special_primes(L, dnum, q0_bits=q0_bits, p_bits=p_bits)
+        self.eng = Engine.product()
+        self.eng.init_params(logn=logn, nlimbs=L, dnum=dnum, nspecial=self.K, slots=slots, q0_bits=q0_bits,
+                             qi_bits=50, p_bits=p_bits, seed=seed)
+        self.eng.lib.gpqhe_set_stream(ctypes.c_void_p(stream.cuda_stream))
+        self.pk, self.sk = self.eng.pk(), self.eng.sk()
+        self.eng.keypair(self.pk, self.sk)
+        self.rk = self.eng.evks(slots)
+        self.eng.genrk(self.rk, self.sk)
+        n = 1 << logn
+        self.n, self.L, self.B, self.s, self.dnum = n, L, batch, slots, self.eng.info.dnum
+        rng = np.random.default_rng(seed)
+        self.M = np.ascontiguousarray((rng.uniform(-1, 1, (slots, slots)) + 1j * rng.uniform(-1, 1, (slots, slots)))
+                                      .ravel())
+        words = 2 * L * n
+        self.x = torch.empty(max(batch, 1) * words, dtype=torch.int64, device="cuda")
+        self.y = torch.empty(max(batch, 1) * 2 * (L - 1) * n, dtype=torch.int64, device="cuda")
+        self.r = torch.empty_like(self.x)
+        torch.cuda.synchronize()
+        for i in range(batch):
+            self.eng.lib.poly_fill_uniform(self.x.data_ptr() + 8 * i * words, 2, L, seed + first + i)
+        self.eng.sync()
+
+    def step(self):
+        self.eng.lib.he_gemv_batch(self.y.data_ptr(), self.M.ctypes.data, self.x.data_ptr(), self.B, self.L, self.rk)
+
+    def rot_step(self):
+        self.eng.lib.he_rot_batch(self.r.data_ptr(), self.x.data_ptr(), self.B, self.L, 1, self.rk)
+
+    def alg_bytes(self):
+        """Per gemv: read the ciphertext (2 L limbs), write the output (2 (L-1)
+        limbs), the s - 1 rotation keys (2 dnum (L+K) limbs each) and the s
+        encoded diagonals (L+K limbs each) amortised over the batch."""
+        n, L, nm = self.n, self.L, self.L + self.K
+        return (2 * L + 2 * (L - 1)) * n * 8 + ((self.s - 1) * 2 * self.dnum * nm + self.s * nm) * n * 8 / self.B
+
+    def rot_alg_bytes(self):
+        n, L, nm = self.n, self.L, self.L + self.K
+        return 4 * L * n * 8 + 2 * self.dnum * nm * n * 8 / self.B
+
+    def close(self):
+        del self.x, self.y, self.r
+        self.eng.free_evks(self.rk)
         self.eng.exit()
 
 
@@ -556,6 +617,144 @@ def shard_check(mine, stream, args, rank, world, backend):
     return res
 
 
+def gemv_cpu_baseline(args, slots):
+    """The oracle's he_gemv_batch (CPU restatement, OpenMP over the batch: one
+    ciphertext per thread) on a bounded sample of the same workload."""
+    import numpy as np
+
+    from hectr_amd.gpqhe import Engine
+    share = int(os.environ.get("OMP_NUM_THREADS", str(min(16, usable_cpus()))))
+    ctypes.CDLL("libgomp.so.1").omp_set_num_threads(share)
+    L, logn = args.nlimbs, args.logn
+    dnum = args.dnum or L
+    K = args.nspecial or special_primes(L, dnum, q0_bits=args.q0_bits, p_bits=args.p_bits)
+    ora = Engine.oracle()
+    ora.init_params(logn=logn, nlimbs=L, dnum=dnum, slots=slots, q0_bits=args.q0_bits, qi_bits=50,
+                    p_bits=args.p_bits, seed=7, nspecial=K)
+    pk, sk = ora.pk(), ora.sk()
+    ora.keypair(pk, sk)
+    rk = ora.evks(slots)
+    ora.genrk(rk, sk)
+    n, cnt = 1 << logn, share
+    rng = np.random.default_rng(7)
+    M = np.ascontiguousarray((rng.uniform(-1, 1, (slots, slots)) + 0j).ravel())
+    x = np.zeros(cnt * 2 * L * n, dtype=np.uint64)
+    y = np.zeros(cnt * 2 * (L - 1) * n, dtype=np.uint64)
+    ora.lib.poly_fill_uniform(x.ctypes.data, 2 * cnt, L, 11)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        ora.lib.he_gemv_batch(y.ctypes.data, M.ctypes.data, x.ctypes.data, cnt, L, rk)
+        done += cnt
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    ora.free_evks(rk)
+    ora.exit()
+    return {"value": done / dt, "unit": "gemv/s", "cores": share, "kind": "port",
+            "sample": f"{done} he_gemv at N=2^{logn}, L={L}, {slots} slots on {share} threads "
+                      f"(batches of {cnt} distinct ciphertexts, {dt:.1f} s)"}
+
+
+def gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
+    """HECTR's encrypted matrix-vector step, he_gemv_batch (north_star: the
+    hempc ciphertext batch; Galois rotation on the hot path), at the
+    headline's ring and prime sizes with HECTR's own slot count, each rank its
+    shard of one global batch under one key; he_rot_batch beside it."""
+    import numpy as np
+    import torch
+    from hectr_amd import dist as hdist
+    B, s = args.gemv_batch, args.gemv_slots
+    steps = max(2, args.steps // 2)
+    L, dnum = args.nlimbs, args.dnum or args.nlimbs
+    gb = GemvBatch(stream, args.logn, L, dnum, args.q0_bits, args.p_bits, args.nspecial, s, B, rank * B,
+                   GEMV_KEY_SEED)
+    t0 = time.perf_counter()
+    gb.step()  # the first call folds the rotation keys with the diagonals (cached)
+    gb.eng.sync()
+    first_s = time.perf_counter() - t0
+    t_mine = timed(gb.step, steps, 1, gb.eng.sync, barrier)
+    t_all = hdist.all_values(t_mine, device=red_dev)
+    t = max(t_all)
+    tr = hdist.max_over_ranks(timed(gb.rot_step, steps, 1, gb.eng.sync, barrier), device=red_dev)
+    gb.eng.prof_enable(True)
+    ti0 = time.perf_counter()
+    for _ in range(steps):
+        gb.step()
+    gb.eng.sync()
+    step_s = (time.perf_counter() - ti0) / steps
+    stats = gb.eng.prof_collect()
+    gb.eng.prof_enable(False)
+    leg = None
+    if rank == 0:
+        v, vr = world * B * steps / t, world * B * steps / tr
+        dom = max(stats, key=lambda k: stats[k][1])
+        launches, tot_us, kbytes = stats[dom]
+        per_launch = B / (launches / steps)
+        alg = gb.alg_bytes()
+        avg_us = tot_us / launches
+        achieved = alg * per_launch / avg_us / 1e3
+        generic = None
+        try:
+            generic = json.load(open(os.path.join(ROOT, "profiles", "r5_gemv_baseline_generic.json")))
+        except (OSError, ValueError):
+            pass
+        leg = {"workload": f"he_gemv_batch ({s} x {s} complex matrix, {s} non-zero diagonals, hoisted rotations), "
+                           f"N=2^{args.logn}, L={L}, K={gb.K}, dnum={gb.dnum}, primes {args.q0_bits}/50/{args.p_bits} "
+                           f"bits, batch={B} ciphertexts per GPU",
+               "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "gemv/s", "steps": steps,
+               "ms_per_step": 1e3 * t / steps, "rank_times_s": t_all, "rank_time_min_s": min(t_all),
+               "rank_time_max_s": t,
+               "rotations_in_gemv_per_s": v * (s - 1), "us_per_gemv_per_gpu": 1e6 * world / v,
+               "first_call_ms": 1e3 * first_s,
+               "rot_batch": {"value": vr, "unit": "rotations/s", "us_per_rotation_per_gpu": 1e6 * world / vr,
+                             "op_roofline_frac": gb.rot_alg_bytes() * vr / world / 1e9 / HBM_PEAK_GBS},
+               "op_roofline": {"alg_bytes_per_op": alg, "achieved_GBs": alg * v / world / 1e9,
+                               "frac": alg * v / world / 1e9 / HBM_PEAK_GBS,
+                               "alg_basis": "read the ciphertext (2 L limbs) + write y (2 (L-1) limbs) + (s-1) "
+                                            "rotation keys and s encoded diagonals / batch"},
+               "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "avg_launch_us": avg_us,
+                            "alg_bytes_per_launch": alg * per_launch, "cts_per_launch": per_launch,
+                            "share_of_step": tot_us / (1e6 * step_s * steps)},
+               "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0], "us_per_gemv": w[1] / (steps * B),
+                               "streamed_GBs": w[2] / w[1] / 1e3}
+                           for k, w in sorted(stats.items(), key=lambda kv: -kv[1][1])},
+               "data": "synthetic random-residue ciphertexts (splitmix64), real rotation keys (he_genrk)"}
+        if generic:
+            leg["generic_path_us_per_gemv"] = generic.get("gemv_batch_us_per_ct")
+            leg["generic_path_source"] = "profiles/r5_gemv_baseline_generic.json (round-4 kernels, same shape)"
+            leg["speedup_vs_generic"] = generic["gemv_batch_us_per_ct"] / leg["us_per_gemv_per_gpu"]
+    shard_y = gb.y.cpu() if args.check_shards else None
+    gb.close()
+    barrier()
+    if args.check_shards:
+        parts = [shard_y]
+        if world > 1:
+            import torch.distributed as dist
+            dev = "cuda" if backend == "nccl" else "cpu"
+            tt = shard_y.to(dev)
+            parts = [torch.empty_like(tt) for _ in range(world)]
+            dist.all_gather(parts, tt)
+            parts = [q.cpu() for q in parts]
+        if rank == 0:
+            ref = GemvBatch(stream, args.logn, L, dnum, args.q0_bits, args.p_bits, args.nspecial, s, world * B, 0,
+                            GEMV_KEY_SEED)
+            ref.step()
+            ref.eng.sync()
+            full = ref.y.cpu()
+            ref.close()
+            got = torch.cat(parts)
+            words = full.numel() // (world * B)
+            bad = (got != full).view(world * B, words).any(dim=1).nonzero().flatten().tolist()
+            leg["shard_check"] = {"cts": world * B, "ranks": world, "bit_exact": not bad, "differing_cts": bad[:16]}
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        leg["cpu_baseline"] = gemv_cpu_baseline(args, s)
+    return leg
+
+
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
@@ -586,7 +785,8 @@ def main():
     eng = mb.eng
     eng.lib.gpqhe_set_streams(args.streams)
     elapsed = timed(mb.step, args.steps, args.warmup, eng.sync, barrier)
-    elapsed = hdist.max_over_ranks(elapsed, device=red_dev)
+    rank_times = hdist.all_values(elapsed, device=red_dev)
+    elapsed = max(rank_times)
     value = world * B * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
 
@@ -639,6 +839,7 @@ def main():
                        "streams": args.streams,
                        "parallelism": f"batch-sharded x{world}"},
             "per_gpu_value": value / world,
+            "rank_times_s": rank_times, "rank_time_min_s": min(rank_times), "rank_time_max_s": elapsed,
             "op_roofline": {"alg_bytes_per_op": alg, "achieved_GBs": alg * value / world / 1e9,
                             "frac": alg * value / world / 1e9 / HBM_PEAK_GBS,
                             "us_per_op": 1e6 * world / value},
@@ -716,6 +917,11 @@ def main():
             if alt5:
                 main5["value_60bit"] = alt5["value"]
                 main5["alt_primes"] = alt5
+
+    if not args.no_gemv:
+        g = gemv_leg(args, stream, rank, world, red_dev, barrier, backend)
+        if rank == 0:
+            result["gemv"] = g
 
     if rank == 0 and world == 1 and not args.no_cstr:
         result["cstr"] = cstr_loop(args.cstr_steps)

@@ -147,26 +147,61 @@ struct GemvWin {
   int16_t yi[GPQHE_MAXMOD / 2][3];  // slot t, digit j: its Dc slot, -1: the own digit (c1 limb t)
   int32_t d[MAXE];                  // rotations of this launch's diagonals, ascending
   uint32_t hm[MAXE];                // g_e^-1 mod 2^LOGB
-  uint32_t i5[MAXE];                // g_e^-1 mod 2^(b+1): output block of a source block
-  uint64_t g[MAXE];                 // g_e mod 2n
+  const uint32_t *tab;              // the launch's orbit table (gemv_tab_kernel)
   GwMods md;
   unsigned E, e0, Etot, accumulate;
   unsigned logn, lvl, nm, count, nseg;
 };
+
+// The orbit table of one launch: row (orb, i), 32 words, for source orbit
+// position i < P of orbit orb (block value e' = +-5^i mod 2^(b+1)): word
+// e < E holds (g_e^-1 C) mod 2^LOGB | kb << 16 for the output block kb that
+// the source feeds through diagonal e (C: that block's constant, see the
+// kernel), word 16 the source's own block.  One scalar row load per step
+// replaces the 64-bit scalar arithmetic per diagonal.
+struct GemvTab {
+  uint64_t g[GemvWin::MAXE], gi[GemvWin::MAXE];  // g_e, g_e^-1 mod 2n
+  unsigned E, logn, logb;
+};
+
+__global__ void __launch_bounds__(256) gemv_tab_kernel(uint32_t *tab, GemvTab ta)
+{
+  const unsigned bb = ta.logn - ta.logb, P = 1u << (bb - 1);
+  const unsigned idx = blockIdx.x * 256 + threadIdx.x, row = idx / 32, w = idx % 32;
+  if (row >= 2 * P)
+    return;
+  const uint64_t emask = (2ull << bb) - 1, nmask2 = (2ull << ta.logn) - 1, mb = (1ull << ta.logb) - 1;
+  uint64_t ev = 1, bse = 5;
+  for (unsigned r = row % P; r; r >>= 1, bse = (bse * bse) & emask)
+    if (r & 1)
+      ev = (ev * bse) & emask;
+  if (row >= P)
+    ev = (emask + 1 - ev) & emask;
+  uint32_t v = 0;
+  if (w == 16) {
+    v = gw_brev((unsigned)(ev >> 1), bb);
+  } else if (w < ta.E) {
+    const uint64_t eo = (ev * ta.gi[w]) & emask;  // the output block's value
+    const uint64_t C = ((ta.g[w] * eo) & nmask2) >> (bb + 1);
+    v = (uint32_t)(((ta.gi[w] & mb) * C) & mb) | (gw_brev((unsigned)(eo >> 1), bb) << 16);
+  }
+  tab[idx] = v;
+}
 
 __device__ __forceinline__ double gw_center(double v, double q)
 {
   return v > 0.5 * q ? v - q : v;
 }
 
+// (W NW key doubles per thread: two waves per SIMD, which the LDS ring of
+// W = 16 allows anyway, leave 256 VGPRs)
 template <int LOGB, int W, int NDIG>
-__global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
+__global__ void __launch_bounds__(1 << LOGB) __attribute__((amdgpu_waves_per_eu(1, W >= 16 ? 2 : W >= 8 ? 4 : 8))) gemv_win_kernel(GemvWin a)
 {
   constexpr int B = 1 << LOGB, NW = 2 * NDIG + 1;
   constexpr unsigned MB = B - 1;
   __shared__ double lacc[W][2][B];
   const unsigned logn = a.logn, bb = logn - LOGB, P = 1u << (bb - 1);
-  const uint64_t emask = (2ull << bb) - 1, nmask2 = (2ull << logn) - 1;
   unsigned grp, p;
   if (!xcd_group(a.count, a.nm * 2 * a.nseg, grp, p))
     return;
@@ -192,21 +227,12 @@ __global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
   const double *Kt = a.K + ((((size_t)t * a.Etot + a.e0) * NW) << logn);
   uint64_t *accp = a.acc + (size_t)p * a.acc_stride + ((size_t)t << logn);
   const size_t apoly = (size_t)a.nm << logn;
+  const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
   // source orbit positions [i0, i1): every diagonal of every owned output
   const unsigned i0 = o0 + dmin, i1 = o1 + dmax;
-  uint64_t es = 1;  // orbit value of position i0: +-5^i0 mod 2^(b+1)
-  {
-    uint64_t bse = 5;
-    for (unsigned r = i0 % P; r; r >>= 1, bse = (bse * bse) & emask)
-      if (r & 1)
-        es = (es * bse) & emask;
-    if (orb)
-      es = (emask + 1 - es) & emask;
-  }
-  auto blk = [&](uint64_t ev) { return gw_brev((unsigned)(ev >> 1), bb); };  // block of odd e: brev((e - 1) / 2)
   uint64_t ny[NDIG], nc0 = 0, nc1 = 0;
-  auto fetch = [&](uint64_t ev) {
-    const size_t off = ((size_t)blk(ev) << LOGB) + th;
+  auto fetch = [&](unsigned kb) {
+    const size_t off = ((size_t)kb << LOGB) + th;
 #pragma unroll
     for (int j = 0; j < NDIG; j++)
       ny[j] = src[j][off];
@@ -216,10 +242,9 @@ __global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
         nc1 = c1s[off];
     }
   };
-  fetch(es);
+  fetch(tabo[(i0 & (P - 1)) * 32 + 16]);
   for (unsigned i = i0; i < i1; i++) {
-    const uint64_t ev = es;
-    es = (es * 5) & emask;
+    const uint32_t *tr = tabo + (i & (P - 1)) * 32;
     // centred (|.| <= q/2): every product below is < 0.875 q in magnitude
     double y[NDIG], c0 = 0, c1 = 0;
 #pragma unroll
@@ -231,36 +256,46 @@ __global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
         c1 = gw_center(f64_from_u52(nc1), q);
     }
     if (i + 1 < i1)
-      fetch(es);
-    const size_t koff = ((size_t)blk(ev) << LOGB) + th;
+      fetch(tabo[((i + 1) & (P - 1)) * 32 + 16]);
+    const size_t koff = ((size_t)tr[16] << LOGB) + th;
+    // every diagonal's key words of this source block, requested at once
+    // (W NW doubles: the LDS ring leaves room for two waves per SIMD at
+    // W = 16, so the registers are there; the L2 latency is paid once per step)
+    double kw[W][NW];
+#pragma unroll
+    for (int e = 0; e < W; e++)
+      if (e < E) {
+        const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+          kw[e][w] = (ident && e == 0 && w < 2 * NDIG) ? 0.0 : kp[(size_t)w << logn];
+      }
 #pragma unroll
     for (int e = 0; e < W; e++) {
       const int o = (int)i - a.d[e];
       if (e >= E || o < (int)o0 || o >= (int)o1)
         continue;
-      const uint64_t eo = (ev * a.i5[e]) & emask;  // the output block's orbit value
-      const unsigned C = (unsigned)(((a.g[e] * eo) & nmask2) >> (bb + 1));
-      const unsigned addr = gw_brev((hj[e] - a.hm[e] * C) & MB, LOGB);
-      const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
+      const uint32_t ent = tr[e];
+      const unsigned addr = gw_brev((hj[e] - ent) & MB, LOGB);
       double s0, s1;
       if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
-        const double kP = kp[(size_t)(2 * NDIG) << logn];
+        const double kP = kw[e][2 * NDIG];
         s0 = qs ? f64_mulmod_h(c0, kP, q, qinv) : 0.0;
         s1 = qs ? f64_mulmod_h(c1, kP, q, qinv) : 0.0;
       } else {
-        s0 = f64_mulmod_h(y[0], kp[0], q, qinv);
-        s1 = f64_mulmod_h(y[0], kp[(size_t)NDIG << logn], q, qinv);
+        s0 = f64_mulmod_h(y[0], kw[e][0], q, qinv);
+        s1 = f64_mulmod_h(y[0], kw[e][NDIG], q, qinv);
 #pragma unroll
         for (int j = 1; j < NDIG; j++) {
           if (j == 2) {  // three digits: fold before the third product (|.| stays < 3.2 q)
             s0 = f64_red(s0, q, qinv);
             s1 = f64_red(s1, q, qinv);
           }
-          s0 += f64_mulmod_h(y[j], kp[(size_t)j << logn], q, qinv);
-          s1 += f64_mulmod_h(y[j], kp[(size_t)(NDIG + j) << logn], q, qinv);
+          s0 += f64_mulmod_h(y[j], kw[e][j], q, qinv);
+          s1 += f64_mulmod_h(y[j], kw[e][NDIG + j], q, qinv);
         }
         if (qs)
-          s0 += f64_mulmod_h(c0, kp[(size_t)(2 * NDIG) << logn], q, qinv);
+          s0 += f64_mulmod_h(c0, kw[e][2 * NDIG], q, qinv);
       }
       const unsigned slot = (unsigned)o & (W - 1);
       if (e > 0) {  // (|acc| <= q/2 + |s| < 2.7 q)
@@ -271,7 +306,7 @@ __global__ void __launch_bounds__(1 << LOGB) gemv_win_kernel(GemvWin a)
         lacc[slot][0][addr] = f64_red(s0, q, qinv);
         lacc[slot][1][addr] = f64_red(s1, q, qinv);
       } else {
-        uint64_t *op = accp + ((size_t)blk(eo) << LOGB) + addr;
+        uint64_t *op = accp + ((size_t)(ent >> 16) << LOGB) + addr;
         if (a.accumulate) {
           s0 = f64_red(s0, q, qinv) + f64_from_u52(op[0]);
           s1 = f64_red(s1, q, qinv) + f64_from_u52(op[apoly]);
@@ -378,49 +413,60 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
 {
   const UpTable &up = k_up_table(lvl);
   const unsigned n = G.n, logn = G.logn, nm = up.nm, ndig = up.ndig, alpha = G.alpha;
-  // compact ModUp slots: digit j's targets outside it, in slot order
+  const GwMods md = gw_mods(lvl);
+  // ModUp digits: the split key switch's ModUp kernels (T1 layout: digit j,
+  // slot t at j nm + t), else the INTT / conversion / NTT sequence below
+  // (compact: digit j's targets outside it, in slot order)
   std::vector<int> yi((size_t)nm * 3, -1);
-  unsigned mods[GPQHE_MAXMOD], S = 0;
-  for (unsigned j = 0; j < ndig; j++) {
-    const unsigned lo = j * alpha, hi = std::min(lo + alpha, lvl);
-    for (unsigned t = 0; t < nm; t++) {
-      if (t >= lo && t < hi)
-        continue;
-      yi[(size_t)t * 3 + j] = (int)S;
-      mods[S++] = t < lvl ? t : G.L + (t - lvl);
-    }
-  }
-  const size_t ys = (size_t)lvl * n, ds = (size_t)S * n, as = 2 * (size_t)nm * n;
+  const size_t ys = (size_t)lvl * n, as = 2 * (size_t)nm * n;
+  size_t ds = (size_t)ndig * nm * n;
   uint64_t *ws = (uint64_t *)pool_alloc((size_t)cnt * (ys + ds + as) * 8);
   uint64_t *ybuf = ws, *Dc = ybuf + cnt * ys, *acc = Dc + cnt * ds;
-  // 1. y = INTT(c1) x n^-1 [(Q_j/q_i)^-1]
-  LimbSet in{}, yo{};
-  in.base = (uint64_t *)x + x_pstride;
-  in.per = lvl;
-  in.count = lvl * cnt;
-  in.stride = x_stride;
-  yo = in;
-  yo.base = ybuf;
-  yo.stride = ys;
-  for (unsigned i = 0; i < lvl; i++)
-    in.mods[i] = yo.mods[i] = (uint8_t)i;
-  k_ntt_ex(in, yo, true, up.ysc);
-  // 2. conversion to every slot outside each digit, 3. their forward NTT
-  const GwMods md = gw_mods(lvl);
-  {
-    ProfScope ps(KC_GEMV_FBC, 8.0 * n * cnt * ((double)lvl + S));
-    hipLaunchKernelGGL(gemv_fbc_kernel, dim3(n / 256, cnt), dim3(256), 0, G.stream, Dc, ds, ybuf, ys, up.cd, md, logn,
-                       lvl, nm, ndig, alpha);
-    HIP_CHECK(hipGetLastError());
+  if (k_modup_c1_split(Dc, ybuf, x, x_stride, x_pstride, cnt, lvl)) {
+    for (unsigned j = 0; j < ndig; j++)
+      for (unsigned t = 0; t < nm; t++)
+        if (!(t >= j * alpha && t < std::min(j * alpha + alpha, lvl)))
+          yi[(size_t)t * 3 + j] = (int)(j * nm + t);
+  } else {
+    unsigned mods[GPQHE_MAXMOD], S = 0;
+    for (unsigned j = 0; j < ndig; j++) {
+      const unsigned lo = j * alpha, hi = std::min(lo + alpha, lvl);
+      for (unsigned t = 0; t < nm; t++) {
+        if (t >= lo && t < hi)
+          continue;
+        yi[(size_t)t * 3 + j] = (int)S;
+        mods[S++] = t < lvl ? t : G.L + (t - lvl);
+      }
+    }
+    ds = (size_t)S * n;  // (within the ndig nm n words reserved per ciphertext)
+    // 1. y = INTT(c1) x n^-1 [(Q_j/q_i)^-1]
+    LimbSet in{}, yo{};
+    in.base = (uint64_t *)x + x_pstride;
+    in.per = lvl;
+    in.count = lvl * cnt;
+    in.stride = x_stride;
+    yo = in;
+    yo.base = ybuf;
+    yo.stride = ys;
+    for (unsigned i = 0; i < lvl; i++)
+      in.mods[i] = yo.mods[i] = (uint8_t)i;
+    k_ntt_ex(in, yo, true, up.ysc);
+    // 2. conversion to every slot outside each digit, 3. their forward NTT
+    {
+      ProfScope ps(KC_GEMV_FBC, 8.0 * n * cnt * ((double)lvl + S));
+      hipLaunchKernelGGL(gemv_fbc_kernel, dim3(n / 256, cnt), dim3(256), 0, G.stream, Dc, ds, ybuf, ys, up.cd, md,
+                         logn, lvl, nm, ndig, alpha);
+      HIP_CHECK(hipGetLastError());
+    }
+    LimbSet dl{};
+    dl.base = Dc;
+    dl.per = S;
+    dl.count = S * cnt;
+    dl.stride = ds;
+    for (unsigned i = 0; i < S; i++)
+      dl.mods[i] = (uint8_t)mods[i];
+    k_ntt(dl, false);
   }
-  LimbSet dl{};
-  dl.base = Dc;
-  dl.per = S;
-  dl.count = S * cnt;
-  dl.stride = ds;
-  for (unsigned i = 0; i < S; i++)
-    dl.mods[i] = (uint8_t)mods[i];
-  k_ntt(dl, false);
   // 4. the inner products, diagonals in groups spanning at most 16 rotations
   constexpr int LOGB = 8;
   const unsigned P = 1u << (logn - LOGB - 1);
@@ -447,22 +493,34 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   a.count = cnt;
   a.nseg = nseg;
   const dim3 grid(xcd_blocks(cnt, nm * 2 * nseg));
+  uint32_t *tab = (uint32_t *)pool_alloc((size_t)2 * P * 32 * 4);
   bool first = true;
   for (unsigned e0 = 0; e0 < E;) {
     unsigned e1 = e0;
-    while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < 16)
+    // (three digits: 7 key words per diagonal in registers; GPQHE_GEMV_SPAN
+    // caps the span for the occupancy A/B: 8 -> a 32 KB ring, four waves per SIMD)
+    static const unsigned span_env = getenv("GPQHE_GEMV_SPAN") ? (unsigned)atoi(getenv("GPQHE_GEMV_SPAN")) : 16;
+    const unsigned span_max = std::min(ndig >= 3 ? 8u : 16u, std::max(1u, span_env));
+    while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < span_max)
       e1++;
     a.E = e1 - e0;
     a.e0 = e0;
     a.accumulate = first ? 0 : 1;
+    GemvTab ta{};
+    ta.E = a.E;
+    ta.logn = logn;
+    ta.logb = LOGB;
     for (unsigned e = 0; e < a.E; e++) {
       uint64_t g, gi;
       gw_galois(d[e0 + e], g, gi);
       a.d[e] = (int32_t)d[e0 + e];
-      a.g[e] = g;
       a.hm[e] = (uint32_t)(gi & ((1u << LOGB) - 1));
-      a.i5[e] = (uint32_t)(gi & ((2ull << (logn - LOGB)) - 1));
+      ta.g[e] = g;
+      ta.gi[e] = gi;
     }
+    hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
+    HIP_CHECK(hipGetLastError());
+    a.tab = tab;
     const unsigned span = d[e1 - 1] - d[e0] + 1;
     {
       // reads each ciphertext's ModUp digits and c0 once, the folded keys once
@@ -478,14 +536,34 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     first = false;
     e0 = e1;
   }
-  // 5. ModDown of both accumulators of every ciphertext
+  pool_free(tab);
+  // 5. ModDown of both accumulators of every ciphertext: the dropped slots'
+  // inverse row pass, then the fused conversion (dn_cols) and combine (dn_rows)
   if (!E)
     HIP_CHECK(hipMemsetAsync(acc, 0, (size_t)cnt * as * 8, G.stream));
+  const unsigned keep = mode == 1 ? lvl - 1 : lvl, nd = nm - keep;
+  const bool fused = k_ks_fused_ok() && nd <= 5;
+  if (fused) {
+    LimbSet dr{};
+    dr.base = acc + ((size_t)keep << logn);
+    dr.per = nd;
+    dr.count = nd * 2 * cnt;
+    dr.stride = (size_t)nm * n;
+    for (unsigned d = 0; d < nd; d++)
+      dr.mods[d] = (uint8_t)(keep + d < lvl ? keep + d : G.L + (keep + d - lvl));
+    k_ntt_rows(dr, dr, true);
+  }
+  auto down = [&](uint64_t *o, uint64_t *X, unsigned npoly) {
+    if (fused)
+      k_moddown_fused(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode);
+    else
+      k_moddown(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode);
+  };
   if (y_stride == 2 * y_pstride) {
-    k_moddown(y, y_pstride, acc, (size_t)nm * n, 2 * cnt, lvl, mode);
+    down(y, acc, 2 * cnt);
   } else {
     for (unsigned c = 0; c < cnt; c++)  // (one ciphertext: an object's own layout)
-      k_moddown(y + c * y_stride, y_pstride, acc + c * as, (size_t)nm * n, 2, lvl, mode);
+      down(y + c * y_stride, acc + c * as, 2);
   }
   pool_free(ws);
 }

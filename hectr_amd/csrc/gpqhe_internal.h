@@ -258,6 +258,10 @@ void k_ntt(const LimbSet &s, bool inverse);
 // out of place (in and out of the same geometry; out may equal in); post: per-slot
 // Shoup pairs replacing n^-1 (inverse only, n >= 2^13)
 void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_t *post);
+// The row pass alone of the two-pass transform (n >= 2^13): what
+// k_moddown_fused expects of the dropped limbs (inverse), or the second half
+// of a forward transform whose column pass ran elsewhere
+void k_ntt_rows(const LimbSet &in, const LimbSet &out, bool inverse);
 void k_binop(uint64_t *out, const uint64_t *a, const uint64_t *b, unsigned npoly, unsigned lvl,
              size_t out_pstride, size_t a_pstride, size_t b_pstride, int op);
 void k_neg(uint64_t *x, unsigned npoly, unsigned lvl, size_t pstride);
@@ -462,6 +466,12 @@ const UpTable &k_up_table(unsigned lvl);  // ModUp conversion tables of a level 
 // (gemv_win.hip): every modulus of basis_qp(lvl) below 2^51, 2^13 <= n <= 2^17,
 // at most three digits
 bool k_gemv_win_ok(unsigned lvl);
+// ModUp of the c1 of count ciphertexts (c0 at x + c x_stride, c1 at + x_pstride)
+// through the split key switch's ModUp kernels: T1 [count][ndig][nm][n] in NTT
+// form on every slot outside its digit (own-digit slots unwritten); ybuf
+// [count][lvl][n] workspace.  False when the ring / prime set has no such form.
+bool k_modup_c1_split(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, size_t x_stride, size_t x_pstride,
+                      unsigned count, unsigned lvl);
 struct GemvDiagIn {
   unsigned d;           // rotation (0: the identity)
   const uint64_t *pt;   // encoded diagonal over basis_qp(lvl) (NTT form); null: 1

@@ -451,6 +451,41 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
   });
 }
 
+// The row pass of the two-pass NTT (n = n1 x 2^LOGN2; ntt2_launch): the
+// batched form when every slot has polys enough to share a workgroup's
+// staged twiddles, else one tile per workgroup.
+template <int LOGN2>
+static void ntt_rows_launch(bool inv, const LimbSet &in, const LimbSet &out)
+{
+  const unsigned logn = G.logn, n = G.n;
+  const unsigned blocks = in.count * (n / 4096);
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  constexpr int QN = 2;
+  const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
+  if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
+    // ~12 polys per quarter stream (two pair ranges per group of 48 polys:
+    // one wave of workgroups): forward 86.6 -> 76.2, inverse 99 -> 96 us per
+    // group against ~4 per quarter; ~24 (107 us inverse) and ~8 were slower,
+    // and a second poly in flight (PF = 2) no faster
+    const unsigned members = std::max(1u, polys / (12 * QN));
+    // inverse: 8-byte staged twiddles (w only, quotient from the product):
+    // 94 VGPRs, no spills (16-byte entries spilled 16 at this launch bound),
+    // 107 -> 98 us per 48-poly group; the forward pass measured 86 -> 88 us
+    // with them and keeps 16-byte (w, w/q) entries
+    // inverse: each thread loads its round-C words directly (16-byte loads,
+    // no transpose through LDS): 94.6 -> 88.4-90.5 us per 48-poly group
+    auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
+    hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw, G.dev.mc,
+                       members);
+  } else if (inv) {
+    hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
+                       G.dev.mc);
+  } else {
+    hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
+                       G.dev.mc);
+  }
+}
+
 template <int LOGT1, int LOGN2>
 static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const uint64_t *post)
 {
@@ -476,32 +511,7 @@ static void ntt2_launch(const LimbSet &s, const LimbSet &o, bool inverse, const 
       hipLaunchKernelGGL((ntt2_cols_kernel<LOGT1, false>), dim3(blocks), dim3(256), 0, G.stream, in, out, logn, tw,
                          G.dev.mc, (const uint64_t *)nullptr);
   };
-  auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) {
-    constexpr int QN = 2;
-    const unsigned polys = in.count / in.per, groups = in.per * (n / 2048);
-    if (polys >= 4 * QN && in.per == out.per) {  // config 2: 7.75 -> 7.50 ms roundtrip
-      // ~12 polys per quarter stream (two pair ranges per group of 48 polys:
-      // one wave of workgroups): forward 86.6 -> 76.2, inverse 99 -> 96 us per
-      // group against ~4 per quarter; ~24 (107 us inverse) and ~8 were slower,
-      // and a second poly in flight (PF = 2) no faster
-      const unsigned members = std::max(1u, polys / (12 * QN));
-      // inverse: 8-byte staged twiddles (w only, quotient from the product):
-      // 94 VGPRs, no spills (16-byte entries spilled 16 at this launch bound),
-      // 107 -> 98 us per 48-poly group; the forward pass measured 86 -> 88 us
-      // with them and keeps 16-byte (w, w/q) entries
-      // inverse: each thread loads its round-C words directly (16-byte loads,
-      // no transpose through LDS): 94.6 -> 88.4-90.5 us per 48-poly group
-      auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
-      hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw,
-                         G.dev.mc, members);
-    } else if (inv) {
-      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
-                         G.dev.mc);
-    } else {
-      hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn,
-                         tw, G.dev.mc);
-    }
-  };
+  auto rows_launch = [&](bool inv, const LimbSet &in, const LimbSet &out) { ntt_rows_launch<LOGN2>(inv, in, out); };
   if (!inverse) {
     {
       ProfScope ps(KC_NTT2_COLS_FWD, pass_bytes);
@@ -546,6 +556,22 @@ void k_ntt_ex(const LimbSet &in, const LimbSet &out, bool inverse, const uint64_
   case 17: ntt2_launch<8, 9>(in, out, inverse, post); return;
   default: gpqhe_die("k_ntt_ex: ring degree 2^%u not supported", G.logn);
   }
+}
+
+void k_ntt_rows(const LimbSet &in, const LimbSet &out, bool inverse)
+{
+  if (!in.count)
+    return;
+  ProfScope ps(inverse ? KC_NTT3_ROWS_INV : KC_NTT3_ROWS_FWD, 16.0 * G.n * in.count);
+  switch (G.logn) {
+  case 13: ntt_rows_launch<7>(inverse, in, out); break;
+  case 14: ntt_rows_launch<7>(inverse, in, out); break;
+  case 15: ntt_rows_launch<8>(inverse, in, out); break;
+  case 16: ntt_rows_launch<8>(inverse, in, out); break;
+  case 17: ntt_rows_launch<9>(inverse, in, out); break;
+  default: gpqhe_die("k_ntt_rows: ring degree 2^%u not supported", G.logn);
+  }
+  HIP_CHECK(hipGetLastError());
 }
 
 // Whole-limb NTT for n = 2^10 .. 2^12 (HECTR's own ring): one block of n/8
@@ -2678,7 +2704,9 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
 // per-tile kernel fetched every twiddle from L2 at every round and waited on
 // one pair's loads at a time (sq_wait_any 0.49).  Same values: canonical
 // outputs of the same exact residue arithmetic.
-template <int LOGN2, int QN>
+// ONE: y = INTT_rows(a1 x s) (b unused): the ModUp of a ciphertext's c1 alone
+// (he_gemv / he_rot batches, k_modup_c1_split)
+template <int LOGN2, int QN, bool ONE = false>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y, const uint64_t *a, const uint64_t *b,
                                                                      size_t in_stride, size_t in_pstride,
                                                                      unsigned logn, unsigned lvl, unsigned count,
@@ -2709,14 +2737,17 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y
   // this thread's 8 consecutive words 8 th + k: its round-C elements
   auto fetch = [&](uint64_t (&A1)[8], uint64_t (&B1)[8], unsigned p) {
     const ulonglong2 *pa = (const ulonglong2 *)(a + p * in_stride + in_pstride + off + 8 * th);
-    const ulonglong2 *pb = (const ulonglong2 *)(b + p * in_stride + in_pstride + off + 8 * th);
+    const ulonglong2 *pb = (const ulonglong2 *)((ONE ? a : b) + p * in_stride + in_pstride + off + 8 * th);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const ulonglong2 x = pa[i], z = pb[i];
+      const ulonglong2 x = pa[i];
       A1[2 * i] = x.x;
       A1[2 * i + 1] = x.y;
-      B1[2 * i] = z.x;
-      B1[2 * i + 1] = z.y;
+      if constexpr (!ONE) {
+        const ulonglong2 z = pb[i];
+        B1[2 * i] = z.x;
+        B1[2 * i + 1] = z.y;
+      }
     }
   };
   unsigned p = pb0 + qi;
@@ -2731,7 +2762,10 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y
       // exact FP64 product of canonical residues, then times the ModUp factor
       // s: |r| <= q/2 after the reduction, so with the recomputed s / q the
       // quotient is off by < 1/2 + 0.75 q 2^-52: |r s - .| < 0.9 q
-      r[k] = f64_mulmod_h(f64_from_u52(nA[k]), f64_from_u52(nB[k]), q, qinv);
+      if constexpr (ONE)
+        r[k] = f64_from_u52(nA[k]);
+      else
+        r[k] = f64_mulmod_h(f64_from_u52(nA[k]), f64_from_u52(nB[k]), q, qinv);
       r[k] = f64_mulmod_h(f64_red(r[k], q, qinv), sd, q, qinv);
     }
     if (p + QN < pb1)
@@ -3810,6 +3844,70 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
   case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
   case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
   default: gpqhe_die("split key switch needs 2^13 <= n <= 2^17");
+  }
+}
+
+// ModUp of the c1 of `count` ciphertexts (he_gemv / he_rot batches,
+// gemv_win.hip) through the split key switch's first two kernels, every
+// modulus below 2^51: y = the inverse row pass of c1 x n^-1 [(Q_j/q_i)^-1]
+// (d2_rows_q_kernel<ONE>), then the column INTT, the conversion and the
+// forward column pass (ks_cols) -> T1 [count][ndig][nm][n] (own-digit slots
+// not written), then the forward row pass of every converted slot: T1 ends in
+// NTT form.  False when this ring / prime set has no such form.
+template <int LOGT1, int LOGN2>
+static bool modup_c1_launch(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, size_t x_stride, size_t x_pstride,
+                            unsigned count, unsigned lvl)
+{
+  const UpTable &up = up_table(lvl);
+  const unsigned nm = up.nm, ndig = up.ndig, n = G.n;
+  const unsigned na_min = lvl - (ndig - 1) * G.alpha;
+  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl));
+  if (!up.f64 || !invc || !GPQHE_D2Q || !G.twd)
+    return false;
+  {
+    const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * 2);
+    constexpr int QN = 2;
+    const unsigned groups = lvl * (n / 2048), members = std::max(1u, count / (12 * QN));
+    hipLaunchKernelGGL((d2_rows_q_kernel<LOGN2, QN, true>), dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0,
+                       G.stream, ybuf, x, (const uint64_t *)nullptr, x_stride, x_pstride, G.logn, lvl, count, members,
+                       tw, G.dev.mc, (const uint64_t *)up.ysc);
+    HIP_CHECK(hipGetLastError());
+  }
+  ks_cols_stage<LOGT1>(ybuf, T1, count, lvl, true);
+  for (unsigned j = 0; j < ndig; j++) {
+    const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, lvl);
+    for (unsigned r = 0; r < 2; r++) {  // the slots before and after the digit
+      const unsigned t0 = r ? hi : 0, t1 = r ? nm : lo;
+      if (t0 >= t1)
+        continue;
+      LimbSet ls{};
+      ls.base = T1 + ((size_t)j * nm + t0) * n;
+      ls.per = t1 - t0;
+      ls.count = ls.per * count;
+      ls.stride = (size_t)ndig * nm * n;
+      for (unsigned t = t0; t < t1; t++)
+        ls.mods[t - t0] = (uint8_t)(t < lvl ? t : G.L + (t - lvl));
+      ProfScope ps(KC_NTT3_ROWS_FWD, 16.0 * n * ls.count);
+      ntt_rows_launch<LOGN2>(false, ls, ls);
+      HIP_CHECK(hipGetLastError());
+    }
+  }
+  return true;
+}
+
+bool k_modup_c1_split(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, size_t x_stride, size_t x_pstride,
+                      unsigned count, unsigned lvl)
+{
+  if (!k_ks_fused_ok() || (lvl + G.alpha - 1) / G.alpha > 3)
+    return false;
+  switch (G.logn) {
+  case 13: return modup_c1_launch<6, 7>(T1, ybuf, x, x_stride, x_pstride, count, lvl);
+  case 14: return modup_c1_launch<7, 7>(T1, ybuf, x, x_stride, x_pstride, count, lvl);
+  case 15: return modup_c1_launch<7, 8>(T1, ybuf, x, x_stride, x_pstride, count, lvl);
+  case 16: return modup_c1_launch<7, 9>(T1, ybuf, x, x_stride, x_pstride, count, lvl);
+  case 17: return modup_c1_launch<8, 9>(T1, ybuf, x, x_stride, x_pstride, count, lvl);
+  default: return false;
   }
 }
 

@@ -53,6 +53,18 @@ def max_over_ranks(x: float, device="cpu") -> float:
     return float(t.item())
 
 
+def all_values(x: float, device="cpu") -> list:
+    """Every rank's value of x, in rank order (one all_gather)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
 def shard(count: int, rank: int, world: int):
     """Contiguous shard [start, stop) of `count` global items for `rank`."""
     base, extra = divmod(count, world)

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${RUN:-stall}
 mkdir -p $OUT
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-B="python bench.py --steps 2 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --alt-bits 0 --streams 1 ${BENCH_ARGS}"
+B=${STALL_CMD:-"python bench.py --steps 2 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --no-gemv --alt-bits 0 --streams 1 ${BENCH_ARGS}"}
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
            "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE" \

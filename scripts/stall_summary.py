@@ -43,6 +43,8 @@ for k, c in per.items():
         out.append(f"avg_waves={d['SQ_LEVEL_WAVES'] / max(d['SQ_BUSY_CYCLES'], 1):.1f}")
     if "SQ_INST_LEVEL_VMEM" in d:
         out.append(f"vmem_lat_q={d['SQ_INST_LEVEL_VMEM'] / max(d.get('SQ_INSTS_VMEM_RD', 0) + d.get('SQ_INSTS_VMEM_WR', 0), 1):.0f}")
+    if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+        out.append(f"l2_hit={d['TCC_HIT_sum'] / max(d['TCC_HIT_sum'] + d['TCC_MISS_sum'], 1):.3f}")
     for n in ("SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL", "SQ_LDS_DATA_FIFO_FULL"):
         if n in d:
             out.append(f"{n[3:].lower()}={d[n] / wc:.3f}")
