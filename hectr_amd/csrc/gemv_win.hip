@@ -33,6 +33,8 @@
 #include "ntt_device.h"
 #include "tables.h"
 
+#include <string.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -150,7 +152,7 @@ struct GemvWin {
   const uint32_t *tab;              // the launch's orbit table (gemv_tab_kernel)
   GwMods md;
   unsigned E, e0, Etot, accumulate;
-  unsigned logn, lvl, nm, count, nseg;
+  unsigned logn, lvl, nm, count, nseg, alpha;
 };
 
 // The orbit table of one launch: row (orb, i), 32 words, for source orbit
@@ -320,6 +322,198 @@ __global__ void __launch_bounds__(1 << LOGB) __attribute__((amdgpu_waves_per_eu(
 }
 
 // ---------------------------------------------------------------------------
+// Output-stationary form (gemv_ows_kernel): blocks of 64 positions, one wave
+// per output block.  A workgroup of 16 waves owns (basis slot, orbit, segment
+// of the orbit) for two ciphertexts and advances along the segment 16 output
+// blocks at a time; the source blocks those outputs read (through every
+// diagonal: o + d_e) sit in an LDS ring of 32 blocks, centred doubles, each
+// loaded from HBM once.  A wave reads its sources straight from the ring at
+// the permuted lane (the within-block map is a permutation of the wave's 64
+// lanes: conflict-free), multiplies by its output positions' key words (one
+// load per key word for both ciphertexts) and keeps both accumulators in
+// registers -- no LDS read-modify-write, one barrier pair per 16 blocks.
+// Keys in output order (fold with ginv = 1).
+// Table row (orb, o): word e = C_{o,e} mod 64, the constant of output block o
+// through diagonal e; word 16 = the block of orbit position o.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) gemv_otab_kernel(uint32_t *tab, GemvTab ta)
+{
+  const unsigned bb = ta.logn - 6, P = 1u << (bb - 1);
+  const unsigned idx = blockIdx.x * 256 + threadIdx.x, row = idx / 32, w = idx % 32;
+  if (row >= 2 * P)
+    return;
+  const uint64_t emask = (2ull << bb) - 1, nmask2 = (2ull << ta.logn) - 1;
+  uint64_t ev = 1, bse = 5;
+  for (unsigned r = row % P; r; r >>= 1, bse = (bse * bse) & emask)
+    if (r & 1)
+      ev = (ev * bse) & emask;
+  if (row >= P)
+    ev = (emask + 1 - ev) & emask;
+  uint32_t v = 0;
+  if (w == 16)
+    v = gw_brev((unsigned)(ev >> 1), bb);
+  else if (w < ta.E)
+    v = (uint32_t)((((ta.g[w] * ev) & nmask2) >> (bb + 1)) & 63);
+  tab[idx] = v;
+}
+
+// C ciphertexts per workgroup share every key word a lane loads (the keys'
+// L2 traffic is the kernel's largest: C = 3 where the ring fits, 144 KB)
+template <int NDIG>
+constexpr int gw_ows_c()
+{
+  return NDIG >= 3 ? 2 : 3;
+}
+
+template <int NDIG, int W>
+__global__ void __launch_bounds__(1024) gemv_ows_kernel(GemvWin a)
+{
+  constexpr int C = gw_ows_c<NDIG>(), RING = 32, NWD = NDIG + 1, NW = 2 * NDIG + 1;
+  __shared__ double ring[C][RING][NWD][64];
+  const unsigned logn = a.logn, bb = logn - 6, P = 1u << (bb - 1);
+  const unsigned nmem = (a.count + C - 1) / C;
+  unsigned grp, mi;
+  if (!xcd_group(nmem, a.nm * 2 * a.nseg, grp, mi))
+    return;
+  const unsigned t = grp / (2 * a.nseg), orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
+  const unsigned SEG = P / a.nseg, o0 = seg * SEG;
+  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
+  const unsigned p0 = mi * C;
+  const unsigned nc = min((unsigned)C, a.count - p0);  // ciphertexts of this workgroup (the last may have fewer)
+  const double q = a.md.q[t], qinv = a.md.qinv[t];
+  const bool qs = t < a.lvl;
+  const int E = (int)a.E, dmin = a.d[0], dmax = a.d[E - 1];
+  const bool ident = dmin == 0;
+  const unsigned jo = qs ? t / a.alpha : 0;  // the own digit's ring word (c1) on a q slot
+  const unsigned jh = gw_brev(L, 6);
+  unsigned gj[W];  // g_e j_hi mod 64
+#pragma unroll
+  for (int e = 0; e < W; e++)
+    gj[e] = e < E ? (a.hm[e] * jh) & 63 : 0;
+  // the ring words: digit j (its ModUp limb, or c1 for the own digit), c0
+  const uint64_t *sp[C][NWD];
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    const unsigned pc = p0 + ((unsigned)c < nc ? c : 0);
+    const uint64_t *xb = a.x + (size_t)pc * a.x_stride;
+#pragma unroll
+    for (int j = 0; j < NDIG; j++) {
+      const int yi = a.yi[t][j];
+      sp[c][j] = yi < 0 ? xb + a.x_pstride + ((size_t)t << logn) : a.Dc + (size_t)pc * a.d_stride + ((size_t)yi << logn);
+    }
+    sp[c][NDIG] = xb + ((size_t)(qs ? t : 0) << logn);
+  }
+  const double *Kt = a.K + ((((size_t)t * a.Etot + a.e0) * NW) << logn);
+  const size_t apoly = (size_t)a.nm << logn;
+  const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
+  uint64_t pv[C][NWD];
+  auto load_src = [&](unsigned s) {
+    const size_t off = ((size_t)tabo[(s & (P - 1)) * 32 + 16] << 6) + L;
+#pragma unroll
+    for (int c = 0; c < C; c++)
+#pragma unroll
+      for (int w = 0; w < NWD; w++)
+        pv[c][w] = (w < NDIG || qs) ? sp[c][w][off] : 0;
+  };
+  auto store_src = [&](unsigned s) {
+    const unsigned slot = s & (RING - 1);
+#pragma unroll
+    for (int c = 0; c < C; c++)
+#pragma unroll
+      for (int w = 0; w < NWD; w++)
+        ring[c][slot][w][L] = gw_center(f64_from_u52(pv[c][w]), q);
+  };
+  const unsigned nadv = SEG / 16;
+  for (unsigned adv = 0; adv < nadv; adv++) {
+    const unsigned ob = o0 + adv * 16;
+    if (adv == 0) {
+      for (unsigned s = ob + dmin + wv; s < ob + 16 + dmax; s += 16) {
+        load_src(s);
+        store_src(s);
+      }
+    } else {
+      store_src(ob + dmax + wv);  // prefetched during the previous advance
+    }
+    __syncthreads();
+    if (adv + 1 < nadv)
+      load_src(ob + 16 + dmax + wv);  // the next advance's new block, in flight meanwhile
+    const unsigned o = ob + wv;
+    const uint32_t *tr = tabo + (o & (P - 1)) * 32;
+    const size_t koff = ((size_t)tr[16] << 6) + L;
+    double a0[C], a1[C];
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      a0[c] = a1[c] = 0.0;
+    // key words two diagonals ahead (a ring of three sets): the L2 latency of
+    // a diagonal's keys overlaps the two before it
+    constexpr int KD = 3;
+    double kw[KD][NW];
+    auto load_keys = [&](int e) {
+      const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
+#pragma unroll
+      for (int w = 0; w < NW; w++)
+        kw[e % KD][w] = (w < 2 * NDIG && !(ident && e == 0)) || (w == 2 * NDIG && qs) ? kp[(size_t)w << logn] : 0.0;
+    };
+#pragma unroll
+    for (int e = 0; e < KD - 1; e++)
+      if (e < E)
+        load_keys(e);
+#pragma unroll
+    for (int e = 0; e < W; e++) {
+      if (e < E) {
+        if (e + KD - 1 < W && e + KD - 1 < E)
+          load_keys(e + KD - 1);
+        const double *k = kw[e % KD];
+        const unsigned slot = (o + a.d[e]) & (RING - 1);
+        const unsigned sl = gw_brev((tr[e] + gj[e]) & 63, 6);  // the lane of this output's source
+        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
+          if (qs) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+              a0[c] = f64_mulmod_h(ring[c][slot][NDIG][sl], k[2 * NDIG], q, qinv);
+              a1[c] = f64_mulmod_h(ring[c][slot][jo][sl], k[2 * NDIG], q, qinv);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < C; c++) {
+            double s0 = a0[c], s1 = a1[c];  // |acc| <= q/2 (+ tiny) between diagonals
+#pragma unroll
+            for (int j = 0; j < NDIG; j++) {
+              const double yv = ring[c][slot][j][sl];
+              if (j == 2) {  // three digits: fold before the third product
+                s0 = f64_red(s0, q, qinv);
+                s1 = f64_red(s1, q, qinv);
+              }
+              s0 += f64_mulmod_h(yv, k[j], q, qinv);
+              s1 += f64_mulmod_h(yv, k[NDIG + j], q, qinv);
+            }
+            if (qs)
+              s0 += f64_mulmod_h(ring[c][slot][NDIG][sl], k[2 * NDIG], q, qinv);
+            a0[c] = f64_red(s0, q, qinv);  // (|s0| < 3.2 q before)
+            a1[c] = f64_red(s1, q, qinv);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      if ((unsigned)c >= nc)
+        continue;
+      uint64_t *op = a.acc + (size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff;
+      double s0 = a0[c], s1 = a1[c];
+      if (a.accumulate) {
+        s0 += f64_from_u52(op[0]);
+        s1 += f64_from_u52(op[apoly]);
+      }
+      op[0] = f64_canon(s0, q, qinv);
+      op[apoly] = f64_canon(s1, q, qinv);
+    }
+    __syncthreads();  // the ring slots the next advance overwrites were read here
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
 static GwMods gw_mods(unsigned lvl)
@@ -364,6 +558,15 @@ static void gw_galois(unsigned d, uint64_t &g, uint64_t &gi)
   gi = gw_pow(5, (ord - d % ord) % ord, mask);
 }
 
+// The inner-product kernel: the output-stationary form (default) or the LDS
+// ring of output blocks (GPQHE_GEMV_KERN=ring, for A/B); it fixes the order
+// the keys are folded in (output / source positions).
+static bool gw_ows()
+{
+  static const bool ows = !(getenv("GPQHE_GEMV_KERN") && !strcmp(getenv("GPQHE_GEMV_KERN"), "ring"));
+  return ows;
+}
+
 size_t k_gemv_fold_words(unsigned E, unsigned lvl)
 {
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
@@ -383,7 +586,7 @@ double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
       gw_galois(dg[e0 + e].d, g, gi);
       fa.pt[e] = dg[e0 + e].pt;
       fa.evk[e] = dg[e0 + e].evk;
-      fa.ginv[e] = gi;
+      fa.ginv[e] = gw_ows() ? 1 : gi;  // output order: no permutation
     }
     ProfScope ps(KC_GEMV_FOLD, 8.0 * G.n * cnt * nm * ((double)(2 * ndig + 1) * 2));
     hipLaunchKernelGGL(gemv_fold_kernel, dim3(G.n / 256, nm, cnt), dim3(256), 0, G.stream, K, fa, E, ndig, G.logn, lvl,
@@ -468,11 +671,18 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     k_ntt(dl, false);
   }
   // 4. the inner products, diagonals in groups spanning at most 16 rotations
-  constexpr int LOGB = 8;
+  const bool ows = gw_ows();
+  const unsigned LOGB = ows ? 6 : 8;
   const unsigned P = 1u << (logn - LOGB - 1);
   unsigned nseg = 1;
-  while (nseg < P / 8 && (size_t)cnt * nm * 2 * nseg < 2048)
-    nseg *= 2;
+  if (ows) {  // segments of >= 16 blocks; enough workgroups to fill the chip
+    const unsigned cw = ndig >= 3 ? 2 : 3;  // gw_ows_c
+    while (nseg < P / 16 && (size_t)nm * 2 * nseg * ((cnt + cw - 1) / cw) < 1024)
+      nseg *= 2;
+  } else {
+    while (nseg < P / 8 && (size_t)cnt * nm * 2 * nseg < 2048)
+      nseg *= 2;
+  }
   GemvWin a{};
   a.x = x;
   a.x_stride = x_stride;
@@ -492,15 +702,17 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   a.nm = nm;
   a.count = cnt;
   a.nseg = nseg;
-  const dim3 grid(xcd_blocks(cnt, nm * 2 * nseg));
+  a.alpha = alpha;
+  const unsigned cpw = ndig >= 3 ? 2 : 3;  // ciphertexts per workgroup (gw_ows_c)
+  const dim3 grid = ows ? dim3(xcd_blocks((cnt + cpw - 1) / cpw, nm * 2 * nseg)) : dim3(xcd_blocks(cnt, nm * 2 * nseg));
   uint32_t *tab = (uint32_t *)pool_alloc((size_t)2 * P * 32 * 4);
   bool first = true;
   for (unsigned e0 = 0; e0 < E;) {
     unsigned e1 = e0;
-    // (three digits: 7 key words per diagonal in registers; GPQHE_GEMV_SPAN
-    // caps the span for the occupancy A/B: 8 -> a 32 KB ring, four waves per SIMD)
+    // (ring form, three digits: 7 key words per diagonal in registers;
+    // GPQHE_GEMV_SPAN caps the span for A/B)
     static const unsigned span_env = getenv("GPQHE_GEMV_SPAN") ? (unsigned)atoi(getenv("GPQHE_GEMV_SPAN")) : 16;
-    const unsigned span_max = std::min(ndig >= 3 ? 8u : 16u, std::max(1u, span_env));
+    const unsigned span_max = std::min(ndig >= 3 && !ows ? 8u : 16u, std::max(1u, span_env));
     while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < span_max)
       e1++;
     a.E = e1 - e0;
@@ -514,11 +726,14 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
       uint64_t g, gi;
       gw_galois(d[e0 + e], g, gi);
       a.d[e] = (int32_t)d[e0 + e];
-      a.hm[e] = (uint32_t)(gi & ((1u << LOGB) - 1));
+      a.hm[e] = (uint32_t)((ows ? g : gi) & ((1u << LOGB) - 1));
       ta.g[e] = g;
       ta.gi[e] = gi;
     }
-    hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
+    if (ows)
+      hipLaunchKernelGGL(gemv_otab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
+    else
+      hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
     HIP_CHECK(hipGetLastError());
     a.tab = tab;
     const unsigned span = d[e1 - 1] - d[e0] + 1;
@@ -527,10 +742,19 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
       // per slot and orbit, writes (or updates) the accumulators
       ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + lvl + (first ? 2.0 : 4.0) * nm) +
                                            (double)a.E * nm * (2 * ndig + 1)));
-      switch (ndig) {
-      case 1: gw_launch<LOGB, 1>(span, grid, a); break;
-      case 2: gw_launch<LOGB, 2>(span, grid, a); break;
-      default: gw_launch<LOGB, 3>(span, grid, a); break;
+      if (ows) {
+        switch (ndig) {
+        case 1: hipLaunchKernelGGL((gemv_ows_kernel<1, 16>), grid, dim3(1024), 0, G.stream, a); break;
+        case 2: hipLaunchKernelGGL((gemv_ows_kernel<2, 16>), grid, dim3(1024), 0, G.stream, a); break;
+        default: hipLaunchKernelGGL((gemv_ows_kernel<3, 16>), grid, dim3(1024), 0, G.stream, a); break;
+        }
+        HIP_CHECK(hipGetLastError());
+      } else {
+        switch (ndig) {
+        case 1: gw_launch<8, 1>(span, grid, a); break;
+        case 2: gw_launch<8, 2>(span, grid, a); break;
+        default: gw_launch<8, 3>(span, grid, a); break;
+        }
       }
     }
     first = false;
