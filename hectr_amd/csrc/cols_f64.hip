@@ -14,12 +14,9 @@
 #ifndef COLSF_PF
 #define COLSF_PF 1
 #endif
-// code size (the kernels exceed the 64 KB instruction cache): 1 -- the column
-// INTTs of the source limbs always on the non-lazy policy (one copy per
-// limb); 2 -- the targets too (one target loop)
-#ifndef COLSF_ONE
-#define COLSF_ONE 0
-#endif
+// (Code size: the kernels exceed the 64 KB instruction cache; one copy of
+// the column INTT / target loop on the non-lazy policy instead of one per
+// policy measured slower, DESIGN 5b, and was removed.)
 
 // ---------------------------------------------------------------------------
 // The INVC ks_cols4 for every modulus below 2^51 (the headline's prime sets):
@@ -156,7 +153,7 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
       ld_limb(i);
     if (!DB && i)
       __syncthreads();  // the previous step's round B has read the tile
-    with_f64c<!DB, COLSF_ONE>(qs[i], twl[i % NB], [&](const auto &ar) {
+    with_f64c<!DB>(qs[i], twl[i % NB], [&](const auto &ar) {
       {
         const int g = th / C;
         double r[16];
@@ -242,15 +239,10 @@ __global__ void __launch_bounds__(256, 2) ks_colsf_kernel(const uint64_t *ybuf, 
         ST_STREAM((uint64_t)__double_as_longlong(r[k]), &(out + (size_t)k * n2)[vo]);
     }(make_f64c<decltype(LZ)::value, !DB>(q, twl[z % NB]));
   };
-  if constexpr (COLSF_ONE >= 2) {
-    for (unsigned v = 0; v < nt; v++)
-      target(v, std::false_type{});
-  } else {
-    for (unsigned v = 0; v < nlz; v++)
-      target(v, std::true_type{});
-    for (unsigned v = nlz; v < nt; v++)
-      target(v, std::false_type{});
-  }
+  for (unsigned v = 0; v < nlz; v++)
+    target(v, std::true_type{});
+  for (unsigned v = nlz; v < nt; v++)
+    target(v, std::false_type{});
 }
 
 // dn_cols_kernel<., ., X5, true, true> for every modulus below 2^51 (the split
@@ -359,7 +351,7 @@ __global__ void __launch_bounds__(256, 2) dn_colsf_kernel(const uint64_t *X, siz
       ld_limb(d);                    // four limbs held it spilled 52 B/lane)
     if (d)
       __syncthreads();  // the previous step's round B has read the tile
-    with_f64c<(LOGT >= 8), COLSF_ONE>(qs[d], twl[d & 1], [&](const auto &ar) {
+    with_f64c<(LOGT >= 8)>(qs[d], twl[d & 1], [&](const auto &ar) {
       {
         const int c = th % C, g = th / C;
         double r[16];
@@ -451,15 +443,10 @@ __global__ void __launch_bounds__(256, 2) dn_colsf_kernel(const uint64_t *X, siz
         ST_STREAM((uint64_t)__double_as_longlong(r[k]), &(out + (size_t)k * n2)[vo]);
     }(make_f64c<decltype(LZ)::value, (LOGT >= 8)>(q, twl[z & 1]));
   };
-  if constexpr (COLSF_ONE >= 2) {
-    for (unsigned v = 0; v < nt; v++)
-      target(v, std::false_type{});
-  } else {
-    for (unsigned v = 0; v < nlz; v++)
-      target(v, std::true_type{});
-    for (unsigned v = nlz; v < nt; v++)
-      target(v, std::false_type{});
-  }
+  for (unsigned v = 0; v < nlz; v++)
+    target(v, std::true_type{});
+  for (unsigned v = nlz; v < nt; v++)
+    target(v, std::false_type{});
 }
 
 

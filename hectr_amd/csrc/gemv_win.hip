@@ -13,23 +13,25 @@
 // residues, so the outputs are the oracle's bit for bit whatever the order of
 // the sums.
 //
-// The inner products.  Diagonal d reads D at the Galois permutation
-// pi_d = auto_index(., 5^d) of each output position.  Blocks of B = 2^LOGB
-// consecutive NTT positions (the top b = logn - LOGB index bits) map to
-// blocks: block e (odd, mod 2^(b+1)) feeds block 5^d e, and inside a block
-// the map is affine in the bit-reversed offset.  The blocks therefore form
-// two orbits under x5 (e = +-5^i), and output block i of an orbit reads
-// source blocks i .. i + dmax.  A workgroup owns (ciphertext, basis slot,
-// orbit) and walks its source blocks in orbit order: each source word is
-// loaded from HBM once, multiplied by every diagonal's key word, and added
-// into a ring of W output blocks of accumulators in LDS (the output position
-// of each product is another thread's, a bijection per diagonal, so one
-// barrier per step suffices); an output block leaves for HBM when its last
-// diagonal has arrived.  The keys are pre-multiplied by their diagonal
-// (pt_d x evk_d, P x pt_d) and stored in source order (gemv_fold_kernel), so
-// a thread's key words are contiguous and shared through L2 by every
-// ciphertext of the batch: the workgroups of one (slot, orbit) are placed on
-// one XCD (xcd_group).
+// The inner products (gemv_win_kernel).  Diagonal d reads D at the Galois
+// permutation pi_d = auto_index(., 5^d) of each output position.  Blocks of
+// 64 consecutive NTT positions (the top b = logn - 6 index bits) map to
+// blocks: block e (odd, mod 2^(b+1)) reads block 5^d e, and inside a block the
+// map is a permutation of the 64 positions, affine in the bit-reversed
+// offset.  The blocks form two orbits under x5 (e = +-5^i), and output block
+// o of an orbit reads source blocks o + d.  One wave owns one output block; a
+// workgroup of 16 waves owns (basis slot, orbit, segment) for three
+// ciphertexts and advances along the segment 16 output blocks at a time.
+// The source blocks those outputs read sit in an LDS ring of 32 blocks
+// (centred doubles), each loaded from HBM once; a wave reads its sources
+// from the ring at the permuted lane (conflict-free: a permutation of its
+// own 64 lanes), multiplies them by its output positions' key words -- one
+// load per word serves the three ciphertexts -- and keeps the accumulators
+// in registers.  The keys are pre-multiplied by their diagonal (pt_d x evk_d,
+// P x pt_d; gemv_fold_kernel) and interleaved per position, so a lane's key
+// words for a diagonal are one 16-byte-aligned run; the workgroups of one
+// (slot, orbit, segment) are placed on one XCD (xcd_group), so they share the
+// keys through its L2.
 #include "ntt_device.h"
 #include "tables.h"
 
@@ -52,9 +54,9 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 }
 
 // ---------------------------------------------------------------------------
-// Folded keys.  K[((t Etot + e) NW + w) n + k'] for source position k' of
-// slot t, which feeds output k = pi_d^-1(k') (NW = 2 ndig + 1):
-//   w < ndig:          [pt_d]_t[k] [b_{d,w}]_t[k]
+// Folded keys, output order, interleaved: K[(((t Etot + e) n + k) KW + w] for
+// output position k of basis slot t (KW = 2 ndig + 2, the last word padding):
+//   w < ndig:           [pt_d]_t[k] [b_{d,w}]_t[k]
 //   ndig <= w < 2 ndig: [pt_d]_t[k] [a_{d,w-ndig}]_t[k]
 //   w = 2 ndig:         [P pt_d]_t[k] on q slots (t < lvl), else 0
 // pt null: 1 (a rotation).  Exact integers below 2^51 as doubles.
@@ -63,30 +65,26 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 struct FoldArgs {
   static constexpr unsigned MAX = 16;
   const uint64_t *pt[MAX], *evk[MAX];
-  uint64_t ginv[MAX];  // g_d^-1 mod 2n
-  unsigned e0;         // the launch's first diagonal in K
+  unsigned e0;  // the launch's first diagonal in K
 };
 
 __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, unsigned Etot, unsigned ndig,
                                                         unsigned logn, unsigned lvl, unsigned L, unsigned nmod,
                                                         const ModConst *mcs)
 {
-  const unsigned kp = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y, e = blockIdx.z;
+  const unsigned k = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y, e = blockIdx.z;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
-  const uint64_t gi = fa.ginv[e];
-  const unsigned k = gi == 1 ? kp : gw_auto_index(kp, gi, logn);
   const uint64_t *pt = fa.pt[e], *ev = fa.evk[e];
   const uint64_t w = pt ? pt[((size_t)t << logn) + k] : 1;
-  const unsigned nw = 2 * ndig + 1;
-  double *o = K + ((((size_t)t * Etot + fa.e0 + e) * nw) << logn) + kp;
+  const unsigned kw = 2 * ndig + 2;
+  double *o = K + ((((size_t)t * Etot + fa.e0 + e) << logn) + k) * kw;
   for (unsigned j = 0; j < ndig; j++) {
-    const uint64_t b = ev ? mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0;
-    const uint64_t a = ev ? mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0;
-    o[(size_t)j << logn] = (double)b;
-    o[(size_t)(ndig + j) << logn] = (double)a;
+    o[j] = ev ? (double)mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0.0;
+    o[ndig + j] = ev ? (double)mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0.0;
   }
-  o[(size_t)(2 * ndig) << logn] = t < lvl ? (double)mul_mod(w, mc.pmod, mc) : 0.0;
+  o[2 * ndig] = t < lvl ? (double)mul_mod(w, mc.pmod, mc) : 0.0;
+  o[2 * ndig + 1] = 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -143,200 +141,37 @@ struct GemvWin {
   size_t x_stride, x_pstride;
   const uint64_t *Dc;  // compact ModUp digits [count][S][n]
   size_t d_stride;
-  const double *K;  // folded keys [nm][Etot][NW][n]
+  const double *K;  // folded keys [nm][Etot][n][2 ndig + 2]
   uint64_t *acc;    // [count][2][nm][n]
   size_t acc_stride;
   int16_t yi[GPQHE_MAXMOD / 2][3];  // slot t, digit j: its Dc slot, -1: the own digit (c1 limb t)
   int32_t d[MAXE];                  // rotations of this launch's diagonals, ascending
-  uint32_t hm[MAXE];                // g_e^-1 mod 2^LOGB
+  uint32_t hm[MAXE];                // g_e mod 64
   const uint32_t *tab;              // the launch's orbit table (gemv_tab_kernel)
   GwMods md;
   unsigned E, e0, Etot, accumulate;
   unsigned logn, lvl, nm, count, nseg, alpha;
 };
 
-// The orbit table of one launch: row (orb, i), 32 words, for source orbit
-// position i < P of orbit orb (block value e' = +-5^i mod 2^(b+1)): word
-// e < E holds (g_e^-1 C) mod 2^LOGB | kb << 16 for the output block kb that
-// the source feeds through diagonal e (C: that block's constant, see the
-// kernel), word 16 the source's own block.  One scalar row load per step
-// replaces the 64-bit scalar arithmetic per diagonal.
 struct GemvTab {
-  uint64_t g[GemvWin::MAXE], gi[GemvWin::MAXE];  // g_e, g_e^-1 mod 2n
-  unsigned E, logn, logb;
+  uint64_t g[GemvWin::MAXE];  // g_e mod 2n
+  unsigned E, logn;
 };
-
-__global__ void __launch_bounds__(256) gemv_tab_kernel(uint32_t *tab, GemvTab ta)
-{
-  const unsigned bb = ta.logn - ta.logb, P = 1u << (bb - 1);
-  const unsigned idx = blockIdx.x * 256 + threadIdx.x, row = idx / 32, w = idx % 32;
-  if (row >= 2 * P)
-    return;
-  const uint64_t emask = (2ull << bb) - 1, nmask2 = (2ull << ta.logn) - 1, mb = (1ull << ta.logb) - 1;
-  uint64_t ev = 1, bse = 5;
-  for (unsigned r = row % P; r; r >>= 1, bse = (bse * bse) & emask)
-    if (r & 1)
-      ev = (ev * bse) & emask;
-  if (row >= P)
-    ev = (emask + 1 - ev) & emask;
-  uint32_t v = 0;
-  if (w == 16) {
-    v = gw_brev((unsigned)(ev >> 1), bb);
-  } else if (w < ta.E) {
-    const uint64_t eo = (ev * ta.gi[w]) & emask;  // the output block's value
-    const uint64_t C = ((ta.g[w] * eo) & nmask2) >> (bb + 1);
-    v = (uint32_t)(((ta.gi[w] & mb) * C) & mb) | (gw_brev((unsigned)(eo >> 1), bb) << 16);
-  }
-  tab[idx] = v;
-}
 
 __device__ __forceinline__ double gw_center(double v, double q)
 {
   return v > 0.5 * q ? v - q : v;
 }
 
-// (W NW key doubles per thread: two waves per SIMD, which the LDS ring of
-// W = 16 allows anyway, leave 256 VGPRs)
-template <int LOGB, int W, int NDIG>
-__global__ void __launch_bounds__(1 << LOGB) __attribute__((amdgpu_waves_per_eu(1, W >= 16 ? 2 : W >= 8 ? 4 : 8))) gemv_win_kernel(GemvWin a)
-{
-  constexpr int B = 1 << LOGB, NW = 2 * NDIG + 1;
-  constexpr unsigned MB = B - 1;
-  __shared__ double lacc[W][2][B];
-  const unsigned logn = a.logn, bb = logn - LOGB, P = 1u << (bb - 1);
-  unsigned grp, p;
-  if (!xcd_group(a.count, a.nm * 2 * a.nseg, grp, p))
-    return;
-  const unsigned t = grp / (2 * a.nseg), orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
-  const unsigned o0 = seg * P / a.nseg, o1 = (seg + 1) * P / a.nseg;  // outputs owned: orbit positions [o0, o1)
-  const double q = a.md.q[t], qinv = a.md.qinv[t];
-  const bool qs = t < a.lvl;
-  const unsigned th = threadIdx.x, jh = gw_brev(th, LOGB);
-  const int E = (int)a.E, dmin = a.d[0], dmax = a.d[E - 1];
-  const bool ident = dmin == 0;
-  unsigned hj[W];  // g_e^-1 j'_hi: the output offset before the block's constant
-#pragma unroll
-  for (int e = 0; e < W; e++)
-    hj[e] = e < E ? (a.hm[e] * jh) & MB : 0;
-  const uint64_t *xb = a.x + (size_t)p * a.x_stride;
-  const uint64_t *src[NDIG];
-#pragma unroll
-  for (int j = 0; j < NDIG; j++) {
-    const int yi = a.yi[t][j];
-    src[j] = yi < 0 ? xb + a.x_pstride + ((size_t)t << logn) : a.Dc + (size_t)p * a.d_stride + ((size_t)yi << logn);
-  }
-  const uint64_t *c0s = xb + ((size_t)t << logn), *c1s = xb + a.x_pstride + ((size_t)t << logn);
-  const double *Kt = a.K + ((((size_t)t * a.Etot + a.e0) * NW) << logn);
-  uint64_t *accp = a.acc + (size_t)p * a.acc_stride + ((size_t)t << logn);
-  const size_t apoly = (size_t)a.nm << logn;
-  const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
-  // source orbit positions [i0, i1): every diagonal of every owned output
-  const unsigned i0 = o0 + dmin, i1 = o1 + dmax;
-  uint64_t ny[NDIG], nc0 = 0, nc1 = 0;
-  auto fetch = [&](unsigned kb) {
-    const size_t off = ((size_t)kb << LOGB) + th;
-#pragma unroll
-    for (int j = 0; j < NDIG; j++)
-      ny[j] = src[j][off];
-    if (qs) {
-      nc0 = c0s[off];
-      if (ident)
-        nc1 = c1s[off];
-    }
-  };
-  fetch(tabo[(i0 & (P - 1)) * 32 + 16]);
-  for (unsigned i = i0; i < i1; i++) {
-    const uint32_t *tr = tabo + (i & (P - 1)) * 32;
-    // centred (|.| <= q/2): every product below is < 0.875 q in magnitude
-    double y[NDIG], c0 = 0, c1 = 0;
-#pragma unroll
-    for (int j = 0; j < NDIG; j++)
-      y[j] = gw_center(f64_from_u52(ny[j]), q);
-    if (qs) {
-      c0 = gw_center(f64_from_u52(nc0), q);
-      if (ident)
-        c1 = gw_center(f64_from_u52(nc1), q);
-    }
-    if (i + 1 < i1)
-      fetch(tabo[((i + 1) & (P - 1)) * 32 + 16]);
-    const size_t koff = ((size_t)tr[16] << LOGB) + th;
-    // every diagonal's key words of this source block, requested at once
-    // (W NW doubles: the LDS ring leaves room for two waves per SIMD at
-    // W = 16, so the registers are there; the L2 latency is paid once per step)
-    double kw[W][NW];
-#pragma unroll
-    for (int e = 0; e < W; e++)
-      if (e < E) {
-        const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
-#pragma unroll
-        for (int w = 0; w < NW; w++)
-          kw[e][w] = (ident && e == 0 && w < 2 * NDIG) ? 0.0 : kp[(size_t)w << logn];
-      }
-#pragma unroll
-    for (int e = 0; e < W; e++) {
-      const int o = (int)i - a.d[e];
-      if (e >= E || o < (int)o0 || o >= (int)o1)
-        continue;
-      const uint32_t ent = tr[e];
-      const unsigned addr = gw_brev((hj[e] - ent) & MB, LOGB);
-      double s0, s1;
-      if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
-        const double kP = kw[e][2 * NDIG];
-        s0 = qs ? f64_mulmod_h(c0, kP, q, qinv) : 0.0;
-        s1 = qs ? f64_mulmod_h(c1, kP, q, qinv) : 0.0;
-      } else {
-        s0 = f64_mulmod_h(y[0], kw[e][0], q, qinv);
-        s1 = f64_mulmod_h(y[0], kw[e][NDIG], q, qinv);
-#pragma unroll
-        for (int j = 1; j < NDIG; j++) {
-          if (j == 2) {  // three digits: fold before the third product (|.| stays < 3.2 q)
-            s0 = f64_red(s0, q, qinv);
-            s1 = f64_red(s1, q, qinv);
-          }
-          s0 += f64_mulmod_h(y[j], kw[e][j], q, qinv);
-          s1 += f64_mulmod_h(y[j], kw[e][NDIG + j], q, qinv);
-        }
-        if (qs)
-          s0 += f64_mulmod_h(c0, kw[e][2 * NDIG], q, qinv);
-      }
-      const unsigned slot = (unsigned)o & (W - 1);
-      if (e > 0) {  // (|acc| <= q/2 + |s| < 2.7 q)
-        s0 += lacc[slot][0][addr];
-        s1 += lacc[slot][1][addr];
-      }
-      if (e < E - 1) {
-        lacc[slot][0][addr] = f64_red(s0, q, qinv);
-        lacc[slot][1][addr] = f64_red(s1, q, qinv);
-      } else {
-        uint64_t *op = accp + ((size_t)(ent >> 16) << LOGB) + addr;
-        if (a.accumulate) {
-          s0 = f64_red(s0, q, qinv) + f64_from_u52(op[0]);
-          s1 = f64_red(s1, q, qinv) + f64_from_u52(op[apoly]);
-        }
-        op[0] = f64_canon(s0, q, qinv);
-        op[apoly] = f64_canon(s1, q, qinv);
-      }
-    }
-    __syncthreads();  // the ring slot written next step was read this step
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Output-stationary form (gemv_ows_kernel): blocks of 64 positions, one wave
-// per output block.  A workgroup of 16 waves owns (basis slot, orbit, segment
-// of the orbit) for two ciphertexts and advances along the segment 16 output
-// blocks at a time; the source blocks those outputs read (through every
-// diagonal: o + d_e) sit in an LDS ring of 32 blocks, centred doubles, each
-// loaded from HBM once.  A wave reads its sources straight from the ring at
-// the permuted lane (the within-block map is a permutation of the wave's 64
-// lanes: conflict-free), multiplies by its output positions' key words (one
-// load per key word for both ciphertexts) and keeps both accumulators in
-// registers -- no LDS read-modify-write, one barrier pair per 16 blocks.
-// Keys in output order (fold with ginv = 1).
-// Table row (orb, o): word e = C_{o,e} mod 64, the constant of output block o
-// through diagonal e; word 16 = the block of orbit position o.
+// The orbit table of one launch (gemv_tab_kernel): row (orb, o), 32 words, for
+// orbit position o of orbit orb (block value e = +-5^o mod 2^(b+1)): word e <
+// E holds C_{o,e} mod 64, the constant of the permutation from output block o
+// to its source through diagonal e (source offset j'_hi = C + g_e j_hi mod
+// 64), word 16 the block of position o.  One scalar row load per output
+// block replaces the 64-bit arithmetic per diagonal.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gemv_otab_kernel(uint32_t *tab, GemvTab ta)
+__global__ void __launch_bounds__(256) gemv_tab_kernel(uint32_t *tab, GemvTab ta)
 {
   const unsigned bb = ta.logn - 6, P = 1u << (bb - 1);
   const unsigned idx = blockIdx.x * 256 + threadIdx.x, row = idx / 32, w = idx % 32;
@@ -360,15 +195,15 @@ __global__ void __launch_bounds__(256) gemv_otab_kernel(uint32_t *tab, GemvTab t
 // C ciphertexts per workgroup share every key word a lane loads (the keys'
 // L2 traffic is the kernel's largest: C = 3 where the ring fits, 144 KB)
 template <int NDIG>
-constexpr int gw_ows_c()
+constexpr int gw_cts()
 {
   return NDIG >= 3 ? 2 : 3;
 }
 
 template <int NDIG, int W>
-__global__ void __launch_bounds__(1024) gemv_ows_kernel(GemvWin a)
+__global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
-  constexpr int C = gw_ows_c<NDIG>(), RING = 32, NWD = NDIG + 1, NW = 2 * NDIG + 1;
+  constexpr int C = gw_cts<NDIG>(), RING = 32, NWD = NDIG + 1, KW = 2 * NDIG + 2;
   __shared__ double ring[C][RING][NWD][64];
   const unsigned logn = a.logn, bb = logn - 6, P = 1u << (bb - 1);
   const unsigned nmem = (a.count + C - 1) / C;
@@ -403,7 +238,7 @@ __global__ void __launch_bounds__(1024) gemv_ows_kernel(GemvWin a)
     }
     sp[c][NDIG] = xb + ((size_t)(qs ? t : 0) << logn);
   }
-  const double *Kt = a.K + ((((size_t)t * a.Etot + a.e0) * NW) << logn);
+  const double *Kt = a.K + (((size_t)t * a.Etot + a.e0) << logn) * KW;
   const size_t apoly = (size_t)a.nm << logn;
   const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
   uint64_t pv[C][NWD];
@@ -447,12 +282,19 @@ __global__ void __launch_bounds__(1024) gemv_ows_kernel(GemvWin a)
     // key words two diagonals ahead (a ring of three sets): the L2 latency of
     // a diagonal's keys overlaps the two before it
     constexpr int KD = 3;
-    double kw[KD][NW];
+    double kw[KD][KW];
     auto load_keys = [&](int e) {
-      const double *kp = Kt + (((size_t)e * NW) << logn) + koff;
+#ifdef GW_EXP_NOKEY  // (timing experiment: every diagonal takes diagonal 0's keys)
+      const double2 *kp = (const double2 *)(Kt + koff * KW);
+#else
+      const double2 *kp = (const double2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
+#endif
 #pragma unroll
-      for (int w = 0; w < NW; w++)
-        kw[e % KD][w] = (w < 2 * NDIG && !(ident && e == 0)) || (w == 2 * NDIG && qs) ? kp[(size_t)w << logn] : 0.0;
+      for (int w = 0; w < KW / 2; w++) {
+        const double2 v = kp[w];
+        kw[e % KD][2 * w] = v.x;
+        kw[e % KD][2 * w + 1] = v.y;
+      }
     };
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
@@ -480,7 +322,11 @@ __global__ void __launch_bounds__(1024) gemv_ows_kernel(GemvWin a)
             double s0 = a0[c], s1 = a1[c];  // |acc| <= q/2 (+ tiny) between diagonals
 #pragma unroll
             for (int j = 0; j < NDIG; j++) {
+#ifdef GW_EXP_NOLDS  // (timing experiment: no ring reads)
+              const double yv = (double)(sl + j + c);
+#else
               const double yv = ring[c][slot][j][sl];
+#endif
               if (j == 2) {  // three digits: fold before the third product
                 s0 = f64_red(s0, q, qinv);
                 s1 = f64_red(s1, q, qinv);
@@ -558,19 +404,10 @@ static void gw_galois(unsigned d, uint64_t &g, uint64_t &gi)
   gi = gw_pow(5, (ord - d % ord) % ord, mask);
 }
 
-// The inner-product kernel: the output-stationary form (default) or the LDS
-// ring of output blocks (GPQHE_GEMV_KERN=ring, for A/B); it fixes the order
-// the keys are folded in (output / source positions).
-static bool gw_ows()
-{
-  static const bool ows = !(getenv("GPQHE_GEMV_KERN") && !strcmp(getenv("GPQHE_GEMV_KERN"), "ring"));
-  return ows;
-}
-
 size_t k_gemv_fold_words(unsigned E, unsigned lvl)
 {
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
-  return (size_t)nm * E * (2 * ndig + 1) * G.n;
+  return (size_t)nm * E * (2 * ndig + 2) * G.n;
 }
 
 double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
@@ -582,32 +419,15 @@ double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
     FoldArgs fa{};
     fa.e0 = e0;
     for (unsigned e = 0; e < cnt; e++) {
-      uint64_t g, gi;
-      gw_galois(dg[e0 + e].d, g, gi);
       fa.pt[e] = dg[e0 + e].pt;
       fa.evk[e] = dg[e0 + e].evk;
-      fa.ginv[e] = gw_ows() ? 1 : gi;  // output order: no permutation
     }
-    ProfScope ps(KC_GEMV_FOLD, 8.0 * G.n * cnt * nm * ((double)(2 * ndig + 1) * 2));
+    ProfScope ps(KC_GEMV_FOLD, 8.0 * G.n * cnt * nm * ((double)(2 * ndig + 1) + (2 * ndig + 2)));
     hipLaunchKernelGGL(gemv_fold_kernel, dim3(G.n / 256, nm, cnt), dim3(256), 0, G.stream, K, fa, E, ndig, G.logn, lvl,
                        G.L, G.nmod, G.dev.mc);
     HIP_CHECK(hipGetLastError());
   }
   return K;
-}
-
-template <int LOGB, int NDIG>
-static void gw_launch(unsigned span, dim3 grid, const GemvWin &a)
-{
-  if (span <= 1)
-    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 1, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
-  else if (span <= 4)
-    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 4, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
-  else if (span <= 8)
-    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 8, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
-  else
-    hipLaunchKernelGGL((gemv_win_kernel<LOGB, 16, NDIG>), grid, dim3(1 << LOGB), 0, G.stream, a);
-  HIP_CHECK(hipGetLastError());
 }
 
 static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uint64_t *x, size_t x_stride,
@@ -670,19 +490,13 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
       dl.mods[i] = (uint8_t)mods[i];
     k_ntt(dl, false);
   }
-  // 4. the inner products, diagonals in groups spanning at most 16 rotations
-  const bool ows = gw_ows();
-  const unsigned LOGB = ows ? 6 : 8;
-  const unsigned P = 1u << (logn - LOGB - 1);
+  // 4. the inner products, diagonals in launches spanning at most 16
+  // rotations (the LDS ring: 16 output blocks and the 15 more sources they
+  // read); segments of >= 16 blocks, enough workgroups to fill the chip
+  const unsigned P = 1u << (logn - 7), cpw = ndig >= 3 ? 2 : 3;  // (cpw: gw_cts)
   unsigned nseg = 1;
-  if (ows) {  // segments of >= 16 blocks; enough workgroups to fill the chip
-    const unsigned cw = ndig >= 3 ? 2 : 3;  // gw_ows_c
-    while (nseg < P / 16 && (size_t)nm * 2 * nseg * ((cnt + cw - 1) / cw) < 1024)
-      nseg *= 2;
-  } else {
-    while (nseg < P / 8 && (size_t)cnt * nm * 2 * nseg < 2048)
-      nseg *= 2;
-  }
+  while (nseg < P / 16 && (size_t)nm * 2 * nseg * ((cnt + cpw - 1) / cpw) < 1024)
+    nseg *= 2;
   GemvWin a{};
   a.x = x;
   a.x_stride = x_stride;
@@ -703,17 +517,12 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   a.count = cnt;
   a.nseg = nseg;
   a.alpha = alpha;
-  const unsigned cpw = ndig >= 3 ? 2 : 3;  // ciphertexts per workgroup (gw_ows_c)
-  const dim3 grid = ows ? dim3(xcd_blocks((cnt + cpw - 1) / cpw, nm * 2 * nseg)) : dim3(xcd_blocks(cnt, nm * 2 * nseg));
+  const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, nm * 2 * nseg));
   uint32_t *tab = (uint32_t *)pool_alloc((size_t)2 * P * 32 * 4);
   bool first = true;
   for (unsigned e0 = 0; e0 < E;) {
     unsigned e1 = e0;
-    // (ring form, three digits: 7 key words per diagonal in registers;
-    // GPQHE_GEMV_SPAN caps the span for A/B)
-    static const unsigned span_env = getenv("GPQHE_GEMV_SPAN") ? (unsigned)atoi(getenv("GPQHE_GEMV_SPAN")) : 16;
-    const unsigned span_max = std::min(ndig >= 3 && !ows ? 8u : 16u, std::max(1u, span_env));
-    while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < span_max)
+    while (e1 < E && e1 - e0 < GemvWin::MAXE && d[e1] - d[e0] < 16)
       e1++;
     a.E = e1 - e0;
     a.e0 = e0;
@@ -721,41 +530,27 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     GemvTab ta{};
     ta.E = a.E;
     ta.logn = logn;
-    ta.logb = LOGB;
     for (unsigned e = 0; e < a.E; e++) {
       uint64_t g, gi;
       gw_galois(d[e0 + e], g, gi);
       a.d[e] = (int32_t)d[e0 + e];
-      a.hm[e] = (uint32_t)((ows ? g : gi) & ((1u << LOGB) - 1));
+      a.hm[e] = (uint32_t)(g & 63);
       ta.g[e] = g;
-      ta.gi[e] = gi;
     }
-    if (ows)
-      hipLaunchKernelGGL(gemv_otab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
-    else
-      hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
+    hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
     HIP_CHECK(hipGetLastError());
     a.tab = tab;
-    const unsigned span = d[e1 - 1] - d[e0] + 1;
     {
       // reads each ciphertext's ModUp digits and c0 once, the folded keys once
       // per slot and orbit, writes (or updates) the accumulators
       ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + lvl + (first ? 2.0 : 4.0) * nm) +
                                            (double)a.E * nm * (2 * ndig + 1)));
-      if (ows) {
-        switch (ndig) {
-        case 1: hipLaunchKernelGGL((gemv_ows_kernel<1, 16>), grid, dim3(1024), 0, G.stream, a); break;
-        case 2: hipLaunchKernelGGL((gemv_ows_kernel<2, 16>), grid, dim3(1024), 0, G.stream, a); break;
-        default: hipLaunchKernelGGL((gemv_ows_kernel<3, 16>), grid, dim3(1024), 0, G.stream, a); break;
-        }
-        HIP_CHECK(hipGetLastError());
-      } else {
-        switch (ndig) {
-        case 1: gw_launch<8, 1>(span, grid, a); break;
-        case 2: gw_launch<8, 2>(span, grid, a); break;
-        default: gw_launch<8, 3>(span, grid, a); break;
-        }
+      switch (ndig) {
+      case 1: hipLaunchKernelGGL((gemv_win_kernel<1, 16>), grid, dim3(1024), 0, G.stream, a); break;
+      case 2: hipLaunchKernelGGL((gemv_win_kernel<2, 16>), grid, dim3(1024), 0, G.stream, a); break;
+      default: hipLaunchKernelGGL((gemv_win_kernel<3, 16>), grid, dim3(1024), 0, G.stream, a); break;
       }
+      HIP_CHECK(hipGetLastError());
     }
     first = false;
     e0 = e1;

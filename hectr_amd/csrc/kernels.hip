@@ -1988,6 +1988,16 @@ __global__ void ks_inner_kernel(uint64_t *acc0, const uint64_t *D, unsigned logn
 // sp.npoly > 0: the last z slice samples the next step's noise instead
 // (SpecAttach): workgroup (x, y) of it covers coefficients [512 b, 512 b + 512)
 // of noise poly b / (n / 512), b = y gridDim.x + x.
+// Test switch GPQHE_SPEC_ATTACH_TAKE=0: no launch takes the attached
+// speculative work, so api.cpp flush_gemvs runs its fallback launches (the
+// path a disagreement between spec_attach's prediction and a launch's own
+// eligibility test would take; tests/test_gpu_parity.py switch off-paths)
+static bool spec_take()
+{
+  static const bool take = !(getenv("GPQHE_SPEC_ATTACH_TAKE") && atoi(getenv("GPQHE_SPEC_ATTACH_TAKE")) == 0);
+  return take;
+}
+
 struct SpecSmp {
   LimbSet dst;
   ChachaKey key;
@@ -2066,7 +2076,7 @@ void k_gemv_inner_jobs(const GemvJobs &jobs, unsigned njobs, unsigned lvl)
   ProfScope ps(KC_GEMV_INNER, 8.0 * G.n * diags * (ndig * nm + 2 * nm + 2 * lvl));
   // the next step's noise sampling rides along in one more z slice (g_sa)
   SpecSmp sp{};
-  if (g_sa.sample && G.n >= 512 && (size_t)g_sa.npoly * (G.n / 512) <= (size_t)(G.n / 64) * nm) {
+  if (g_sa.sample && spec_take() && G.n >= 512 && (size_t)g_sa.npoly * (G.n / 512) <= (size_t)(G.n / 64) * nm) {
     sp.dst = g_sa.noise;
     sp.key = G.key;
     sp.stream = g_sa.stream;
@@ -2534,7 +2544,7 @@ __global__ void __launch_bounds__(256, 3) ks_rows_kernel(const uint64_t *T1, siz
 template <int LOGT1>
 static bool colsm_ks_ok(unsigned targets)
 {
-  return GPQHE_COLSM && ((targets <= 8 && LOGT1 <= 7) || (GPQHE_COLSM_MB && LOGT1 <= 8));
+  return GPQHE_COLSM && targets <= 8 && LOGT1 <= 7;
 }
 
 static bool ks_colsf_ok(const UpTable &tab, unsigned lvl)
@@ -2705,7 +2715,12 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
 // one pair's loads at a time (sq_wait_any 0.49).  Same values: canonical
 // outputs of the same exact residue arithmetic.
 // ONE: y = INTT_rows(a1 x s) (b unused): the ModUp of a ciphertext's c1 alone
-// (he_gemv / he_rot batches, k_modup_c1_split)
+// (he_gemv / he_rot batches, k_modup_c1_split).
+// Launch bound: hip-clang reads the second argument as amdgpu_waves_per_eu, so
+// 2 QN = 4 waves per SIMD caps the kernel at 128 VGPRs; it needs 114-118 (QN =
+// 2, LOGN2 7-9; 96-100 for ONE) with no spills (-Rpass-analysis=
+// kernel-resource-usage), and two 512-thread workgroups per CU are its
+// intended occupancy.
 template <int LOGN2, int QN, bool ONE = false>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y, const uint64_t *a, const uint64_t *b,
                                                                      size_t in_stride, size_t in_pstride,
@@ -3363,7 +3378,7 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
       // the next step's speculative transforms and ModUp ride along (g_sa)
       SpecNtt sn{};
       unsigned xn = 0;
-      if (g_sa.ntt && !g_sa.sample) {  // (transforms only of noise already sampled in stream order)
+      if (g_sa.ntt && !g_sa.sample && spec_take()) {  // (transforms only of noise already sampled in stream order)
         sn.s = g_sa.noise;
         xn = g_sa.noise.count;
         g_sa.ntt = false;
@@ -3693,7 +3708,7 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
                         tw);
       else if (tab.f64 && FBC64_DN)
         tab.nd <= 4 ? go(dn_cols_kernel<LOGT1, NT, false, true, true>) : go(dn_cols_kernel<LOGT1, NT, true, true, true>);
-      else if (GPQHE_COLSM && (LOGT1 <= 7 || GPQHE_COLSM_DN8))  // (T = 256: 92 B/lane of spills, GPQHE_COLSM_DN8)
+      else if (GPQHE_COLSM && LOGT1 <= 7)  // (T = 256 spilled 92 B/lane and ran slower: not used)
         dn_colsm_launch(LOGT1, dim3(xcd_blocks(members, ngroups)), X, x_pstride, x_off, conv, lvl, members, ngroups, tab,
                         tw);
       else

@@ -6,11 +6,6 @@
 #include <algorithm>
 #include <numeric>
 
-// ksq_kernel<keep> on FP64 prime sets: loads issued one phase ahead (below);
-// -DKSQ_KEEP_PF=0 builds the load-before-use form (same-box A/B)
-#ifndef KSQ_KEEP_PF
-#define KSQ_KEEP_PF 0
-#endif
 // pair streams of ksq_kernel<drop> on FP64 prime sets (3: 168 VGPRs, 2: 256)
 #ifndef KSQ_DROP_QN
 #define KSQ_DROP_QN 3
@@ -24,13 +19,6 @@
 #endif
 // three-digit keys, dropped slots: 2 = forward row twiddles staged (16 KB),
 // the inverse ones from L2; 0 = both from L2
-// FP64 slots: one kernel per lazy-reduction policy (AR 3 / 4), the slots
-// launched in runs of one policy; 0: the policy chosen per slot at run time
-// (AR 1), which the compiler if-converts -- both reductions computed, one
-// selected -- so every slot paid the non-lazy cost
-#ifndef KSQ_LZ_CT
-#define KSQ_LZ_CT 0
-#endif
 // grids of whole waves of workgroups (ksq_launch): same box, single stream,
 // keep 1855 -> 1824-1848, drop 1159 -> 1105-1116 us per chunk; two streams
 // (whose kernels fill each other's tails) unchanged.  0 off, 2 shorter ranges
@@ -82,29 +70,11 @@
 // output word sits where the same pair's input word of the same slot was
 // (he_mul(c, c, b)): the thread that writes it has read it.
 // ===========================================================================
-// streamed operand loads (T1, inputs, conv: each word read once per kernel)
-// as non-temporal loads: measured slower (keep 1853 -> 2140 us per chunk: a
-// thread's two input halves share cache lines), off
-#ifndef KSQ_NT_LD
-#define KSQ_NT_LD 0
-#endif
-typedef uint64_t ksq_u64x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint64_t ksq_ld(const uint64_t *p)
-{
-  if constexpr (KSQ_NT_LD)
-    return __builtin_nontemporal_load(p);
-  else
-    return *p;
-}
-__device__ __forceinline__ ulonglong2 ksq_ld2(const ulonglong2 *p)
-{
-  if constexpr (KSQ_NT_LD) {
-    const ksq_u64x2 v = __builtin_nontemporal_load((const ksq_u64x2 *)p);
-    return make_ulonglong2(v.x, v.y);
-  } else {
-    return *p;
-  }
-}
+// (Measured non-levers, removed: non-temporal loads of the streamed operands
+// -- keep 1853 -> 2140 us per chunk, a thread's two input halves share cache
+// lines; loads one phase ahead in the kept slots' kernel -- 1868 -> 1960 /
+// 2215 us, spills; one kernel per lazy-reduction policy with the slots
+// launched in runs of one policy -- keep 1869, drop 1213 us.  DESIGN 5b.)
 
 // the policy with its lazy-reduction choice fixed (LZ 0 / 1; -1 as it is)
 template <int LZ>
@@ -177,7 +147,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     const uint64_t *s = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      x[k] = ksq_ld(&s[(row << LOGN2) + l + T::TA * k]);
+      x[k] = s[(row << LOGN2) + l + T::TA * k];
   };
   unsigned p = pb0 + qi;
   uint64_t xn[NX > 0 ? NX : 1][8];
@@ -244,7 +214,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int a = 0; a < 4; a++) {
           const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4 * h);
-          const ulonglong2 w0 = ksq_ld2(&v2[0]), w1 = ksq_ld2(&v2[1]);
+          const ulonglong2 w0 = v2[0], w1 = v2[1];
           inw[a][0] = w0.x;
           inw[a][1] = w0.y;
           inw[a][2] = w1.x;
@@ -265,22 +235,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
             cvw[half][k] = cv[(row << LOGN2) + l + T::TA * k];
         }
       }
-      // KEEP_PF (kept slots, FP64): every load one phase ahead -- the first
-      // input half before the converted limb's row pass, the second input half
-      // and each conv half while the previous phase computes -- instead of
-      // each load right before its use (sq_wait_any 0.45)
-      constexpr int KPL = KEEP && ALLF ? KSQ_KEEP_PF : 0;  // 1: the first input half only
-      constexpr bool KPF = KPL >= 2;
-      uint64_t inw2[KPF ? 4 : 1][4], cva[KPF ? 8 : 1], cvb[KPF ? 8 : 1];
-      auto ld_cv = [&](uint64_t (&w)[KPF ? 8 : 1], int half) {
-        if constexpr (KPF) {
-          const uint64_t *cv = conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff;
-#pragma unroll
-          for (int k = 0; k < 8; k++)
-            w[k] = ksq_ld(&cv[(row << LOGN2) + l + T::TA * k]);
-        }
-      };
-      if ((EARLY || KPL) && jo < NDIG)
+      if (EARLY && jo < NDIG)
         ld_in(0);
 #pragma unroll
       for (int u = 0; u < NX; u++) {
@@ -327,24 +282,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
           const double Pd = f64_from_u52(kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            if constexpr (KPF) {
-              if (h == 0) {  // the second half's words into their own registers
-#pragma unroll
-                for (int a = 0; a < 4; a++) {
-                  const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4);
-                  const ulonglong2 w0 = ksq_ld2(&v2[0]), w1 = ksq_ld2(&v2[1]);
-                  inw2[a][0] = w0.x;
-                  inw2[a][1] = w0.y;
-                  inw2[a][2] = w1.x;
-                  inw2[a][3] = w1.y;
-                }
-              } else {
-                ld_cv(cva, 0);
-              }
-            } else if (h || !(EARLY || KPL)) {
+            if (h || !EARLY)
               ld_in(h);
-            }
-            auto iw = [&](int a, int e) { return KPF && h ? inw2[KPF ? a : 0][e] : inw[a][e]; };
+            auto iw = [&](int a, int e) { return inw[a][e]; };
 #pragma unroll
             for (int e = 0; e < 4; e++) {
               const int k = 4 * h + e;
@@ -397,17 +337,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
           const unsigned poly = 2 * p + half;
           const uint64_t *cv = conv + (((size_t)poly * cv_n + t) << logn) + toff;
           V r[8];
-          if constexpr (KPF) {
-            if (half == 0)
-              ld_cv(cvb, 1);  // the second half's conv words, in flight meanwhile
 #pragma unroll
-            for (int k = 0; k < 8; k++)
-              r[k] = A::load_lazy(half ? cvb[k] : cva[k]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-              r[k] = A::load_lazy(EARLY ? cvw[half][k] : ksq_ld(&cv[(row << LOGN2) + l + T::TA * k]));  // conv (lazy)
-          }
+          for (int k = 0; k < 8; k++)
+            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           // out = f D^-1 - NTTrows(conv D^-1): both factors already folded in
@@ -488,20 +420,12 @@ static void ksq_launch(bool keep_stage, const uint64_t *T1, const D01Src &d01, c
   HIP_CHECK(hipGetLastError());
 }
 
-// f(integral_constant<AR>) for an FP64 class: 3 / 4 (KSQ_LZ_CT) or 1
+// f(integral_constant<AR>) for the FP64 class (AR 1: the lazy-reduction
+// policy chosen per slot at run time)
 template <class F>
-static void with_f64_class(int ar, F &&f)
+static void with_f64_class(int, F &&f)
 {
-  if constexpr (KSQ_LZ_CT) {
-    if (ar == 3)
-      f(std::integral_constant<int, 3>{});
-    else if (ar == 4)
-      f(std::integral_constant<int, 4>{});
-    else
-      gpqhe_die("split key switch: FP64 class %d", ar);
-  } else {
-    f(std::integral_constant<int, 1>{});
-  }
+  f(std::integral_constant<int, 1>{});
 }
 
 // ar: the slots' arithmetic class (ksq_kernel AR)
@@ -569,7 +493,7 @@ static void ksq_stage(unsigned ndig, bool allf, bool keep_stage, const uint64_t 
                       const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
                       const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
 {
-  if ((allf && !KSQ_LZ_CT) || (!allf && !KSQ_SPLIT_AR) || ndig == 1) {
+  if (allf || !KSQ_SPLIT_AR || ndig == 1) {
     ksq_dispatch<LOGN2>(ndig, allf ? 1 : 0, keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm,
                         t_lo, t_n, t_n);
     return;
@@ -578,7 +502,7 @@ static void ksq_stage(unsigned ndig, bool allf, bool keep_stage, const uint64_t 
     const unsigned m = t < lvl ? t : G.L + (t - lvl);
     if (!(G.twd != nullptr && G.q[m] < (1ull << 51)))
       return 2;
-    return !KSQ_LZ_CT ? 1 : G.q[m] < (1ull << 50) ? 3 : 4;
+    return 1;
   };
   for (unsigned a = t_lo; a < t_lo + t_n;) {
     const int c = cls(a);

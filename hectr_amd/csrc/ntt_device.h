@@ -1208,15 +1208,8 @@ void ntt2_colsf_launch(int logt, bool inv, unsigned blocks, const LimbSet &in, c
 // cols_mixed.hip: the same for prime sets mixing FP64 and wider integer
 // moduli (GPQHE_COLSM; replaces ks_cols4_kernel<., 8, true, false> and
 // dn_cols_kernel<., 8, ., false, true>)
-// GPQHE_COLSM_MB: more targets than one block's 8 (config 5: 12) as target
-// batches, each re-running the digit's column INTT, instead of a separate
-// column pass of y; GPQHE_COLSM_DN8: dn_colsm at T = 256 too
-#ifndef GPQHE_COLSM_MB
-#define GPQHE_COLSM_MB 0
-#endif
-#ifndef GPQHE_COLSM_DN8
-#define GPQHE_COLSM_DN8 0
-#endif
+// (Measured non-levers, removed: more targets than one block's 8 as target
+// batches re-running the column INTT, and dn_colsm at T = 256)
 #ifndef GPQHE_COLSM
 #define GPQHE_COLSM 1
 #endif

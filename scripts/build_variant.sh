@@ -14,7 +14,7 @@ B=/tmp/gpqhe_var_$NAME
 mkdir -p $B hectr_amd/lib_var/$NAME
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result $EXTRA"
 pids=()
-for f in kernels.hip ks_split.hip cols_f64.hip cols_mixed.hip host_math.cpp api.cpp; do
+for f in kernels.hip ks_split.hip cols_f64.hip cols_mixed.hip gemv_win.hip host_math.cpp api.cpp; do
   /opt/rocm/bin/hipcc $FLAGS -x hip -c $SRC/$f -o $B/$f.o &
   pids+=($!)
 done

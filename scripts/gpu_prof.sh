@@ -12,8 +12,8 @@ if [ -z "$NO_FULL" ]; then
 fi
 # the kernel-trace pass runs the bench's own steps / warmup, so its mean launch
 # time is the one the bench line's roofline uses; PMC passes run short
-BK="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr --no-ntt --no-c5 --alt-bits 0 --streams 1"
-B="python bench.py --steps 3 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --alt-bits 0 --streams 1"
+BK="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr --no-ntt --no-c5 --no-gemv --alt-bits 0 --streams 1"
+B="python bench.py --steps 3 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --no-gemv --alt-bits 0 --streams 1"
 N="python scripts/prof_ntt.py 1024"
 pass() {  # pass <dir> <rocprofv3 args...>  (on the bench command, then on the NTT leg)
   d=$1; shift

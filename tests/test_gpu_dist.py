@@ -22,7 +22,7 @@ def test_bench_two_ranks_shards_bit_exact(streams):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env["HECTR_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
-           "1", "--streams", str(streams), "--no-cpu", "--no-cstr", "--no-ntt", "--no-c5", "--alt-bits", "0",
+           "1", "--streams", str(streams), "--no-cpu", "--no-cstr", "--no-ntt", "--no-c5", "--no-gemv", "--alt-bits", "0",
            "--check-shards"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
@@ -33,3 +33,25 @@ def test_bench_two_ranks_shards_bit_exact(streams):
     chk = d["shard_check"]
     assert chk["pairs"] == 6 and chk["ranks"] == 2
     assert chk["bit_exact"], chk
+
+
+def test_bench_two_ranks_c5_and_gemv_shards_bit_exact():
+    """The config-5 leg (N=2^17, L=12, dnum=3: 3 pairs per rank, split 1 + 2
+    over the two sub-chunk streams) and the gemv leg (he_gemv_batch at the
+    headline shape with HECTR's 16 slots, 3 ciphertexts per rank) at two
+    ranks: each leg's gathered output shards equal one context's run of its
+    whole global batch, and the line reports every rank's time."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
+           "1", "--no-cpu", "--no-cstr", "--no-ntt", "--alt-bits", "0", "--c5-batch", "3", "--gemv-batch", "3",
+           "--check-shards"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert d["shard_check"]["bit_exact"], d["shard_check"]
+    assert len(d["rank_times_s"]) == 2
+    c5, g = d["config5"], d["gemv"]
+    assert c5["shard_check"] == {"pairs": 6, "ranks": 2, "bit_exact": True, "differing_pairs": []}, c5["shard_check"]
+    assert g["shard_check"] == {"cts": 6, "ranks": 2, "bit_exact": True, "differing_cts": []}, g["shard_check"]
+    assert len(c5["rank_times_s"]) == 2 and len(g["rank_times_s"]) == 2

@@ -46,6 +46,11 @@ PARAMS = {
     # rows) and n=2^15 (128 x 256 columns, 256-element rows)
     "c14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
     "c15": ("params", dict(logn=15, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=60, qi_bits=48, p_bits=60)),
+    # all-FP64 sets at n=2^13 and 2^15: the FP64 column kernels
+    # ks_colsf<6, 8> / dn_colsf<6, .> / ntt2_colsf<6, .> (T = 64) and the
+    # n=2^15 split-key-switch forms on every-modulus-below-2^51 primes
+    "f13": ("params", dict(logn=13, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
+    "f15": ("params", dict(logn=15, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
     # one digit of 5 limbs (alpha > 4: the single-target ks_cols_kernel and the
     # streaming ks_rows_kernel), n=2^13, L=5, dnum=1, K=4 (P 240 > 200 bits)
     "a5": ("params", dict(logn=13, nlimbs=5, nspecial=4, dnum=1, slots=64, q0_bits=40, qi_bits=40, p_bits=60)),
@@ -149,7 +154,7 @@ def test_evaluation_ops(oracle, product, name):
         assert np.abs(got - want).max() < 1e-6 * max(1.0, np.abs(want).max()), op
 
 
-@pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c5f", "c14", "c15"])
+@pytest.mark.parametrize("name", ["bench", "bench51", "c5", "c5f", "c14", "c15", "f13", "f15"])
 @pytest.mark.parametrize("npolys", [4, 24])
 def test_ntt_batch_bitexact(oracle, product, name, npolys):
     """Config 2 layout (n=2^16, L=8) and the n=2^17, L=12 chain: forward, then
@@ -178,14 +183,16 @@ def test_ntt_batch_bitexact(oracle, product, name, npolys):
     assert np.array_equal(host, orig)
 
 
-@pytest.mark.parametrize("name,npolys", [("bench51", 1024), ("bench", 97)])
+@pytest.mark.parametrize("name,npolys", [("bench51", 1024), ("bench", 113)])
 def test_ntt_batch_full_shape(oracle, product, name, npolys):
     """Config 2 at its full shape (1024 polys x 8 limbs at
-    N=2^16, the bench's prime set) and 97 polys on the 60-bit set: ntt_batch
-    runs the batch in groups of 48 polys (api.cpp ntt_batch), so these cover
-    every group offset, the row pass's member split at a full group and a
-    partial last group (97 = 48 + 48 + 1).  Forward and inverse are each
-    compared residue by residue with the oracle, not only the roundtrip."""
+    N=2^16, the bench's prime set) and 113 polys on the 60-bit set: ntt_batch
+    runs the batch in groups of 224 MiB (api.cpp ntt_batch: 56 polys of 8
+    limbs at this shape), so these cover every group offset, the row pass's
+    member split at a full group and a one-poly last group (113 = 56 + 56 +
+    1), which the inverse batch (GPQHE_NTT_REV) visits first.  Forward and
+    inverse are each compared residue by residue with the oracle, not only
+    the roundtrip."""
     import torch
     init_both(oracle, product, name)
     n, L = product.n, product.L
@@ -238,7 +245,8 @@ def mul_batch_both(oracle, product, name, cnt, lvl=None, seeds=(1, 2)):
     return out_o, got
 
 
-@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c5f", "c17", "c14", "c15", "a5"])
+@pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c5f", "c17", "c14", "c15", "f13", "f15",
+                                  "a5"])
 def test_mul_rescale_batch_bitexact(oracle, product, name):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 through the streaming inner
     product, the bench's dnum=2/K=4 with 60-bit and with < 2^51 primes), the
@@ -258,9 +266,10 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     5-8 pairs per workgroup, two or three per quarter stream: the next pair's
     prefetch, the key tile shared by the quarters and reused across pairs,
     the accumulator restart), 17 pairs in chunks of 5/5/5/2 (the multi-chunk
-    loop, a short last chunk) and the bench's own 256 pairs (two 128-pair
-    chunks of the 8 GiB workspace, about 3 pairs per quarter), every output
-    residue compared with the oracle.  Also 17 pairs of config 5 (n=2^17, L=12,
+    loop, a short last chunk) and the bench's own 256 pairs (one chunk of the
+    8 GiB workspace as two 128-pair sub-chunks on two streams, about 3 pairs
+    per quarter), every output residue compared with the oracle.  Also 17
+    pairs of config 5 (n=2^17, L=12,
     the three-digit split key switch), config 5's own bench shape (64 pairs per
     GPU, bench.py's c5 leg: its pair ranges and member split), both on the
     60-bit q0/P set and on the headline's all-FP64 prime sizes (c5f), and 17 of c15
@@ -630,7 +639,7 @@ def test_rekey_between_speculative_steps(oracle, product):
 
 
 @pytest.mark.parametrize("switch", ["GPQHE_SPEC", "GPQHE_SPEC_ATTACH", "GPQHE_SPEC_EARLY", "GPQHE_DEFER",
-                                    "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV"])
+                                    "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV", "GPQHE_SPEC_ATTACH_TAKE"])
 def test_small_n_switch_off_paths(switch):
     """Each small-N switch is read once per process (api.cpp static const), so
     its off path runs in a child process (one at a time, nothing else on the
