@@ -429,13 +429,15 @@ D01Src k_mul_keyswitch_fused(uint64_t *acc, uint64_t *d2, uint64_t *ybuf, uint64
 // conversion, then the kept slots' inner product with the ModDown epilogue).
 // out may equal a or b only with one pair and out_pstride == in_pstride.
 bool k_mul_split_ok(unsigned lvl);
-extern hipEvent_t g_split_after_d2;  // recorded after d2_rows when set (experiment)
 // ws: a workspace of k_mul_split_ws_words(count, lvl, rescale) words, or null
 // (the pool's, on the engine stream)
 size_t k_mul_split_ws_words(unsigned count, unsigned lvl, bool rescale);
+// s0, s1: run only stages [s0, s1) (0 d2_rows, 1 ks_cols, 2 ksq<drop>, 3
+// dn_cols, 4 ksq<keep>) -- a batch split into sub-chunks on several streams
+// issues them in its own order; a stage range needs the caller's ws
 void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
                        size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale,
-                       uint64_t *ws = nullptr);
+                       uint64_t *ws = nullptr, int s0 = 0, int s1 = 5);
 // ModDown (mode 0: / P, 1: / P q_{lvl-1}) of X whose drop limbs hold the
 // inverse row pass of their NTT form (k_mul_keyswitch_fused with drop_lo =
 // keep).

@@ -3781,15 +3781,13 @@ bool k_mul_split_ok(unsigned lvl)
   return k_ks_fused_ok() && split_ndig_ok(ndig);
 }
 
-hipEvent_t g_split_after_d2 = nullptr;
-#ifndef GPQHE_SPLIT_SHIFT
-#define GPQHE_SPLIT_SHIFT 1
-#endif
-
+// Stages [s0, s1) of the split key switch (0 d2_rows, 1 ks_cols, 2
+// ksq<drop>, 3 dn_cols, 4 ksq<keep>) on the engine stream; ws is the chunk's
+// workspace (k_mul_split_ws_words), or null for all five stages from the pool.
 template <int LOGT1, int LOGN2>
 static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b,
                              size_t in_stride, size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl,
-                             bool rescale, uint64_t *ws)
+                             bool rescale, uint64_t *ws, int s0, int s1)
 {
   const UpTable &up = up_table(lvl);
   const DownTable &dn = down_table(lvl, rescale ? 1 : 0);
@@ -3802,6 +3800,8 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl) || (!up.f64 && colsm_ks_ok<LOGT1>(nm - na_min)));
   // workspace: the caller's (k_mul_split_ws_words) or the pool's
   const bool own = !ws;
+  if (own && (s0 != 0 || s1 != 5))
+    gpqhe_die("split key switch: a stage range needs the caller's workspace");
   if (own)
     ws = (uint64_t *)pool_alloc(k_mul_split_ws_words(count, lvl, rescale) * 8);
   uint64_t *y = ws;
@@ -3810,30 +3810,28 @@ static void mul_split_launch(uint64_t *out, size_t out_pstride, const uint64_t *
   uint64_t *conv = accd + (size_t)2 * count * nd * n;
   const D01Src d01{a, b, in_stride, in_pstride};
   const bool allf = up.f64 && dn.f64;
-  // (two-stream sub-chunks, api.cpp: the second starts when this one has run
-  // GPQHE_SPLIT_SHIFT stages -- 1: d2_rows, 2: + ks_cols)
-  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 0)
-    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
-  d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc);
-  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 1)
-    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
-  ks_cols_stage<LOGT1>(y, T1, count, lvl, invc);
-  if (g_split_after_d2 && GPQHE_SPLIT_SHIFT == 2)
-    HIP_CHECK(hipEventRecord(g_split_after_d2, G.stream));
-  {
-    // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per
-    // workgroup; writes the inverse row pass of the nd dropped slots
-    ProfScope ps(KC_KSQ_DROP, 8.0 * n * count * ((double)ndig * nd + 2.0 * nd + (rescale ? 4.0 - 1.0 : 0.0)));
-    ksq_run(LOGN2, ndig, allf, false, T1, d01, evkm, accd, (size_t)nd * n, nullptr, dn.ksc, dn.kps, count, lvl,
-            nm, keep, nd);
-  }
-  dn_cols_stage<LOGT1>(conv, accd, (size_t)nd * n, 0, 2 * count, lvl, dn, true);
-  {
-    // reads T1 (ndig - 1 converted limbs), the four input limbs and the two
-    // conv limbs per pair and kept slot; writes the two output limbs
-    ProfScope ps(KC_KSQ_KEEP, 8.0 * n * count * keep * ((double)ndig - 1.0 + 4.0 + 2.0 + 2.0));
-    ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.ksc, dn.kps, count, lvl, nm, 0,
-            keep);
+  for (int st = s0; st < s1; st++) {
+    switch (st) {
+    case 0: d2_intt_launch<LOGT1, LOGN2>(nullptr, y, a, b, in_stride, in_pstride, count, lvl, up, !invc); break;
+    case 1: ks_cols_stage<LOGT1>(y, T1, count, lvl, invc); break;
+    case 2: {
+      // reads T1 (+ the inputs on a dropped q slot) per pair, the key once per
+      // workgroup; writes the inverse row pass of the nd dropped slots
+      ProfScope ps(KC_KSQ_DROP, 8.0 * n * count * ((double)ndig * nd + 2.0 * nd + (rescale ? 4.0 - 1.0 : 0.0)));
+      ksq_run(LOGN2, ndig, allf, false, T1, d01, evkm, accd, (size_t)nd * n, nullptr, dn.ksc, dn.kps, count, lvl,
+              nm, keep, nd);
+      break;
+    }
+    case 3: dn_cols_stage<LOGT1>(conv, accd, (size_t)nd * n, 0, 2 * count, lvl, dn, true); break;
+    case 4: {
+      // reads T1 (ndig - 1 converted limbs), the four input limbs and the two
+      // conv limbs per pair and kept slot; writes the two output limbs
+      ProfScope ps(KC_KSQ_KEEP, 8.0 * n * count * keep * ((double)ndig - 1.0 + 4.0 + 2.0 + 2.0));
+      ksq_run(LOGN2, ndig, allf, true, T1, d01, evkm, out, out_pstride, conv, dn.ksc, dn.kps, count, lvl, nm, 0,
+              keep);
+      break;
+    }
+    }
   }
   if (own)
     pool_free(ws);
@@ -3847,17 +3845,18 @@ size_t k_mul_split_ws_words(unsigned count, unsigned lvl, bool rescale)
 }
 
 void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, const uint64_t *b, size_t in_stride,
-                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale, uint64_t *ws)
+                       size_t in_pstride, const uint64_t *evkm, unsigned count, unsigned lvl, bool rescale, uint64_t *ws,
+                       int s0, int s1)
 {
   switch (G.logn) {
-  case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
-  case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
-  case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
+  case 13: mul_split_launch<6, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws, s0, s1); break;
+  case 14: mul_split_launch<7, 7>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws, s0, s1); break;
+  case 15: mul_split_launch<7, 8>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws, s0, s1); break;
   // 2^16 = 128 x 512: one NTT stage moves from the VALU-bound column kernels
   // to the row passes of the memory-bound ksq kernels (41.5-41.9k -> 42.0k
   // ct-mult/s against 256 x 256, same box)
-  case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
-  case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws); break;
+  case 16: mul_split_launch<7, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws, s0, s1); break;
+  case 17: mul_split_launch<8, 9>(out, out_pstride, a, b, in_stride, in_pstride, evkm, count, lvl, rescale, ws, s0, s1); break;
   default: gpqhe_die("split key switch needs 2^13 <= n <= 2^17");
   }
 }
