@@ -737,6 +737,31 @@ def gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
     shard_y = gb.y.cpu() if args.check_shards else None
     gb.close()
     barrier()
+    if args.alt_bits and args.alt_bits != args.q0_bits:
+        # the same batch at HECTR-like prime sizes (60-bit q0 / P: those slots
+        # on the integer form of the inner-product kernel, the mixed-set ModUp /
+        # ModDown kernels)
+        ga = GemvBatch(stream, args.logn, L, dnum, args.alt_bits, args.alt_bits, 0, s, B, rank * B, GEMV_KEY_SEED)
+        ga.step()
+        ga.eng.sync()
+        ta = hdist.max_over_ranks(timed(ga.step, steps, 1, ga.eng.sync, barrier), device=red_dev)
+        tra = hdist.max_over_ranks(timed(ga.rot_step, steps, 1, ga.eng.sync, barrier), device=red_dev)
+        ga.eng.prof_enable(True)
+        for _ in range(steps):
+            ga.step()
+        ga.eng.sync()
+        sta = ga.eng.prof_collect()
+        ga.eng.prof_enable(False)
+        if rank == 0:
+            va, vra = world * B * steps / ta, world * B * steps / tra
+            leg["alt_primes"] = {
+                "q0_bits": args.alt_bits, "qi_bits": 50, "p_bits": args.alt_bits, "K": ga.K, "value": va,
+                "unit": "gemv/s", "us_per_gemv_per_gpu": 1e6 * world / va,
+                "rot_batch": {"value": vra, "unit": "rotations/s", "us_per_rotation_per_gpu": 1e6 * world / vra},
+                "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0], "us_per_gemv": w[1] / (steps * B)}
+                            for k, w in sorted(sta.items(), key=lambda kv: -kv[1][1])}}
+        ga.close()
+        barrier()
     if args.check_shards:
         def gemv_ref(count):
             ref = GemvBatch(stream, args.logn, L, dnum, args.q0_bits, args.p_bits, args.nspecial, s, count, 0,

@@ -2315,38 +2315,31 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const uint64_t *oend = out + count * out_stride, *aend = a + count * in_stride, *bend = b + count * in_stride;
   const bool alias = (out < aend && a < oend) || (out < bend && b < oend);
   // (GPQHE_SPLIT_PIPE = K >= 2, experiment: K sub-chunks with the HBM-bound
-  // stages (d2_rows, ksq<keep>) on one stream and the VALU-bound ones
-  // (ks_cols, ksq<drop>, dn_cols) on another, issued so that sub-chunk k + 1's
-  // d2_rows and sub-chunk k - 1's keep can run beside sub-chunk k's column
-  // kernels; GPQHE_SPLIT_HCU = c gives the HBM stream c CUs of every XCD's
-  // 32 by a CU mask and the other stream the rest)
-  static const unsigned pipe = env_u("GPQHE_SPLIT_PIPE", 0), hcu = env_u("GPQHE_SPLIT_HCU", 0);
+  // stages (d2_rows, ksq<keep>) on the engine stream and the VALU-bound ones
+  // (ks_cols, ksq<drop>, dn_cols) on the second stream, issued so that
+  // sub-chunk k + 1's d2_rows and sub-chunk k - 1's keep can run beside
+  // sub-chunk k's column kernels.  The two streams are the default mode's
+  // two: a stream beyond the runtime's hardware queues (GPU_MAX_HW_QUEUES,
+  // 4) shares a queue with another and serializes behind it -- the first
+  // form of this experiment, on two streams of its own, measured no kernel
+  // overlap at all in its kernel trace.)
+  static const unsigned pipe = env_u("GPQHE_SPLIT_PIPE", 0);
   const bool split2 = count >= 2 && nchunks == 1 && !alias && k_mul_split_ok(lvl) && rlk->reserved &&
                       rlk->dnum == G.dnum;
   const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
-  if (split2 && pipe >= 2 && pipe <= 8 && count >= pipe) {
-    static hipStream_t sh = nullptr, sv = nullptr;
-    static hipEvent_t evf, evj, eva[8], evb[8];
-    if (!sh) {
-      if (hcu) {
-        // mask bit i: CU i in the order the runtime enumerates them; every
-        // XCD's first hcu of 32 for the HBM stream (XCD-major order assumed)
-        uint32_t mh[8] = {0}, mv[8] = {0};
-        for (unsigned cu = 0; cu < 256; cu++)
-          ((cu % 32) < hcu ? mh : mv)[cu / 32] |= 1u << (cu % 32);
-        HIP_CHECK(hipExtStreamCreateWithCUMask(&sh, 8, mh));
-        HIP_CHECK(hipExtStreamCreateWithCUMask(&sv, 8, mv));
-      } else {
-        HIP_CHECK(hipStreamCreateWithFlags(&sh, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&sv, hipStreamNonBlocking));
-      }
-      HIP_CHECK(hipEventCreateWithFlags(&evf, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&evj, hipEventDisableTiming));
-      for (unsigned k = 0; k < 8; k++) {
-        HIP_CHECK(hipEventCreateWithFlags(&eva[k], hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&evb[k], hipEventDisableTiming));
-      }
+  static hipStream_t s2 = nullptr;
+  static hipEvent_t ev_fork, ev_d2, ev_join, eva[8], evb[8];
+  if (split2 && (nsub == 2 || pipe >= 2) && !s2) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_d2, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    for (unsigned k = 0; k < 8; k++) {
+      HIP_CHECK(hipEventCreateWithFlags(&eva[k], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&evb[k], hipEventDisableTiming));
     }
+  }
+  if (split2 && pipe >= 2 && pipe <= 8 && count >= pipe) {
     std::vector<std::unique_ptr<Ws>> ws;
     std::vector<size_t> lo(pipe + 1);
     for (unsigned k = 0; k <= pipe; k++)
@@ -2354,44 +2347,31 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
     for (unsigned k = 0; k < pipe; k++)
       ws.emplace_back(new Ws(k_mul_split_ws_words((unsigned)(lo[k + 1] - lo[k]), lvl, true)));
     const hipStream_t eng = G.stream;
-    HIP_CHECK(hipEventRecord(evf, eng));
-    HIP_CHECK(hipStreamWaitEvent(sh, evf, 0));
-    HIP_CHECK(hipStreamWaitEvent(sv, evf, 0));
+    HIP_CHECK(hipEventRecord(ev_fork, eng));
+    HIP_CHECK(hipStreamWaitEvent(s2, ev_fork, 0));
     auto run = [&](unsigned k, int s0, int s1) {
       const unsigned c = (unsigned)(lo[k + 1] - lo[k]);
       k_mul_relin_split(out + lo[k] * out_stride, (lvl - 1) * n, a + lo[k] * in_stride, b + lo[k] * in_stride,
                         in_stride, lvl * n, evkm, c, lvl, true, ws[k]->p, s0, s1);
     };
-    G.stream = sh;
     for (unsigned k = 0; k < pipe; k++) {
       run(k, 0, 1);
-      HIP_CHECK(hipEventRecord(eva[k], sh));
+      HIP_CHECK(hipEventRecord(eva[k], eng));
     }
-    G.stream = sv;
+    G.stream = s2;
     for (unsigned k = 0; k < pipe; k++) {
-      HIP_CHECK(hipStreamWaitEvent(sv, eva[k], 0));
+      HIP_CHECK(hipStreamWaitEvent(s2, eva[k], 0));
       run(k, 1, 4);
-      HIP_CHECK(hipEventRecord(evb[k], sv));
+      HIP_CHECK(hipEventRecord(evb[k], s2));
     }
-    G.stream = sh;
+    G.stream = eng;
     for (unsigned k = 0; k < pipe; k++) {
-      HIP_CHECK(hipStreamWaitEvent(sh, evb[k], 0));
+      HIP_CHECK(hipStreamWaitEvent(eng, evb[k], 0));
       run(k, 4, 5);
     }
-    HIP_CHECK(hipEventRecord(evj, sh));
-    G.stream = eng;
-    HIP_CHECK(hipStreamWaitEvent(eng, evj, 0));
     return;
   }
   if (nsub == 2 && split2) {
-    static hipStream_t s2 = nullptr;
-    static hipEvent_t ev_fork, ev_d2, ev_join;
-    if (!s2) {
-      HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-      HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&ev_d2, hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-    }
     const unsigned c1 = (unsigned)(count / 2), c2 = (unsigned)(count - c1);
     // both workspaces come from the engine stream's pool before the fork and
     // go back to it after the join

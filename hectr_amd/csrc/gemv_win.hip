@@ -65,7 +65,8 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 struct FoldArgs {
   static constexpr unsigned MAX = 16;
   const uint64_t *pt[MAX], *evk[MAX];
-  unsigned e0;  // the launch's first diagonal in K
+  unsigned e0;       // the launch's first diagonal in K
+  uint64_t intmask;  // bit t: basis slot t on 64-bit integer arithmetic (modulus >= 2^51)
 };
 
 __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, unsigned Etot, unsigned ndig,
@@ -78,13 +79,19 @@ __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, 
   const uint64_t *pt = fa.pt[e], *ev = fa.evk[e];
   const uint64_t w = pt ? pt[((size_t)t << logn) + k] : 1;
   const unsigned kw = 2 * ndig + 2;
+  const bool isint = (fa.intmask >> t) & 1;
+  // FP64 slots: the residue as a double; integer slots: its Montgomery form
+  // x 2^64 mod q (bits), so the kernel's REDC of y x returns y x mod q
+  auto put = [&](double *o, uint64_t v) {
+    *(uint64_t *)o = isint ? mul_mod(v, mc.r64, mc) : (uint64_t)__double_as_longlong((double)v);
+  };
   double *o = K + ((((size_t)t * Etot + fa.e0 + e) << logn) + k) * kw;
   for (unsigned j = 0; j < ndig; j++) {
-    o[j] = ev ? (double)mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0.0;
-    o[ndig + j] = ev ? (double)mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0.0;
+    put(o + j, ev ? mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0);
+    put(o + ndig + j, ev ? mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0);
   }
-  o[2 * ndig] = t < lvl ? (double)mul_mod(w, mc.pmod, mc) : 0.0;
-  o[2 * ndig + 1] = 0.0;
+  put(o + 2 * ndig, t < lvl ? mul_mod(w, mc.pmod, mc) : 0);
+  put(o + 2 * ndig + 1, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -95,6 +102,7 @@ __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, 
 // ---------------------------------------------------------------------------
 struct GwMods {
   double q[GPQHE_MAXMOD / 2], qinv[GPQHE_MAXMOD / 2];  // per basis slot of basis_qp(lvl)
+  uint64_t qi[GPQHE_MAXMOD / 2], qni[GPQHE_MAXMOD / 2];  // the same as integers, -q^-1 mod 2^64
 };
 
 __global__ void __launch_bounds__(256) gemv_fbc_kernel(uint64_t *Dc, size_t d_stride, const uint64_t *y,
@@ -149,6 +157,8 @@ struct GemvWin {
   uint32_t hm[MAXE];                // g_e mod 64
   const uint32_t *tab;              // the launch's orbit table (gemv_tab_kernel)
   GwMods md;
+  uint8_t slot[GPQHE_MAXMOD / 2];   // the launch's basis slots (one arithmetic class)
+  unsigned ns;
   unsigned E, e0, Etot, accumulate;
   unsigned logn, lvl, nm, count, nseg, alpha;
 };
@@ -200,22 +210,49 @@ constexpr int gw_cts()
   return NDIG >= 3 ? 2 : 3;
 }
 
-template <int NDIG, int W>
+// One ring word: a centred double (FP64 slots) or a canonical residue
+// (integer slots).
+union GwWord {
+  double d;
+  uint64_t u;
+};
+
+// Montgomery REDC of a 128-bit sum v < q 2^64: v 2^-64 mod q in [0, 2q)
+__device__ __forceinline__ uint64_t gw_redc(uint64_t hi, uint64_t lo, uint64_t q, uint64_t qni)
+{
+  return hi + mulhi64(lo * qni, q) + (lo != 0);
+}
+
+// (hi:lo) += y w
+__device__ __forceinline__ void gw_mac128(uint64_t &hi, uint64_t &lo, uint64_t y, uint64_t w)
+{
+  const uint64_t pl = y * w, ph = mulhi64(y, w);
+  lo += pl;
+  hi += ph + (lo < pl);
+}
+
+// INT: the slots of this launch are on 64-bit integer moduli (q >= 2^51: the
+// 60-bit q_0 / P of HECTR-like prime sets).  Their key words are Montgomery
+// forms (gemv_fold_kernel), a diagonal's products are summed in 128 bits
+// (at most 2 ndig + 1 < 2^4 products of residues below q < 2^60: below
+// q 2^64) and reduced by one REDC, the accumulators kept in [0, 2q).
+template <int NDIG, int W, bool INT>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
   constexpr int C = gw_cts<NDIG>(), RING = 32, NWD = NDIG + 1, KW = 2 * NDIG + 2;
-  __shared__ double ring[C][RING][NWD][64];
+  __shared__ GwWord ring[C][RING][NWD][64];
   const unsigned logn = a.logn, bb = logn - 6, P = 1u << (bb - 1);
   const unsigned nmem = (a.count + C - 1) / C;
   unsigned grp, mi;
-  if (!xcd_group(nmem, a.nm * 2 * a.nseg, grp, mi))
+  if (!xcd_group(nmem, a.ns * 2 * a.nseg, grp, mi))
     return;
-  const unsigned t = grp / (2 * a.nseg), orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
+  const unsigned t = a.slot[grp / (2 * a.nseg)], orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
   const unsigned SEG = P / a.nseg, o0 = seg * SEG;
   const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
   const unsigned p0 = mi * C;
   const unsigned nc = min((unsigned)C, a.count - p0);  // ciphertexts of this workgroup (the last may have fewer)
   const double q = a.md.q[t], qinv = a.md.qinv[t];
+  const uint64_t qi = a.md.qi[t], qni = a.md.qni[t], q2 = 2 * qi;
   const bool qs = t < a.lvl;
   const int E = (int)a.E, dmin = a.d[0], dmax = a.d[E - 1];
   const bool ident = dmin == 0;
@@ -255,8 +292,12 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 #pragma unroll
     for (int c = 0; c < C; c++)
 #pragma unroll
-      for (int w = 0; w < NWD; w++)
-        ring[c][slot][w][L] = gw_center(f64_from_u52(pv[c][w]), q);
+      for (int w = 0; w < NWD; w++) {
+        if constexpr (INT)
+          ring[c][slot][w][L].u = pv[c][w];
+        else
+          ring[c][slot][w][L].d = gw_center(f64_from_u52(pv[c][w]), q);
+      }
   };
   const unsigned nadv = SEG / 16;
   for (unsigned adv = 0; adv < nadv; adv++) {
@@ -275,45 +316,96 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     const unsigned o = ob + wv;
     const uint32_t *tr = tabo + (o & (P - 1)) * 32;
     const size_t koff = ((size_t)tr[16] << 6) + L;
+    // accumulators: |.| <= q/2 (+ tiny) between diagonals (FP64), [0, 2q) (INT)
     double a0[C], a1[C];
+    uint64_t u0[C], u1[C];
 #pragma unroll
-    for (int c = 0; c < C; c++)
+    for (int c = 0; c < C; c++) {
       a0[c] = a1[c] = 0.0;
+      u0[c] = u1[c] = 0;
+    }
+    if constexpr (INT) {
+      // one diagonal at a time (the body is too long to unroll over 16: a
+      // register array indexed by the diagonal would go to scratch); the
+      // next diagonal's key words in flight meanwhile
+      uint64_t kc[KW], kn[KW];
+      auto load_keys = [&](int e, uint64_t (&kk)[KW]) {
+        const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
+#pragma unroll
+        for (int w = 0; w < KW / 2; w++) {
+          const ulonglong2 v = kp[w];
+          kk[2 * w] = v.x;
+          kk[2 * w + 1] = v.y;
+        }
+      };
+      load_keys(0, kn);
+      for (int e = 0; e < E; e++) {
+#pragma unroll
+        for (int w = 0; w < KW; w++)
+          kc[w] = kn[w];
+        if (e + 1 < E)
+          load_keys(e + 1, kn);
+        const unsigned slot = (o + a.d[e]) & (RING - 1);
+        const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
+        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
+          if (qs) {
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+              const uint64_t y0 = ring[c][slot][NDIG][sl].u, y1 = ring[c][slot][jo][sl].u;
+              u0[c] = gw_redc(mulhi64(y0, kc[2 * NDIG]), y0 * kc[2 * NDIG], qi, qni);
+              u1[c] = gw_redc(mulhi64(y1, kc[2 * NDIG]), y1 * kc[2 * NDIG], qi, qni);
+            }
+          }
+          continue;
+        }
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+          uint64_t h0 = 0, l0 = 0, h1 = 0, l1 = 0;
+#pragma unroll
+          for (int j = 0; j < NDIG; j++) {
+            const uint64_t yv = ring[c][slot][j][sl].u;
+            gw_mac128(h0, l0, yv, kc[j]);
+            gw_mac128(h1, l1, yv, kc[NDIG + j]);
+          }
+          if (qs)
+            gw_mac128(h0, l0, ring[c][slot][NDIG][sl].u, kc[2 * NDIG]);
+          u0[c] = lazy_lt2q(u0[c] + gw_redc(h0, l0, qi, qni), q2);
+          u1[c] = lazy_lt2q(u1[c] + gw_redc(h1, l1, qi, qni), q2);
+        }
+      }
+    }
     // key words two diagonals ahead (a ring of three sets): the L2 latency of
     // a diagonal's keys overlaps the two before it
     constexpr int KD = 3;
-    double kw[KD][KW];
+    uint64_t kw[KD][KW];
     auto load_keys = [&](int e) {
-#ifdef GW_EXP_NOKEY  // (timing experiment: every diagonal takes diagonal 0's keys)
-      const double2 *kp = (const double2 *)(Kt + koff * KW);
-#else
-      const double2 *kp = (const double2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
-#endif
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
 #pragma unroll
       for (int w = 0; w < KW / 2; w++) {
-        const double2 v = kp[w];
+        const ulonglong2 v = kp[w];
         kw[e % KD][2 * w] = v.x;
         kw[e % KD][2 * w + 1] = v.y;
       }
     };
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
-      if (e < E)
+      if (!INT && e < E)
         load_keys(e);
 #pragma unroll
     for (int e = 0; e < W; e++) {
-      if (e < E) {
+      if (!INT && e < E) {
         if (e + KD - 1 < W && e + KD - 1 < E)
           load_keys(e + KD - 1);
-        const double *k = kw[e % KD];
+        const uint64_t *ku = kw[e % KD];
+        auto k = [&](int w) { return __longlong_as_double((long long)ku[w]); };
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + gj[e]) & 63, 6);  // the lane of this output's source
         if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
           if (qs) {
 #pragma unroll
             for (int c = 0; c < C; c++) {
-              a0[c] = f64_mulmod_h(ring[c][slot][NDIG][sl], k[2 * NDIG], q, qinv);
-              a1[c] = f64_mulmod_h(ring[c][slot][jo][sl], k[2 * NDIG], q, qinv);
+              a0[c] = f64_mulmod_h(ring[c][slot][NDIG][sl].d, k(2 * NDIG), q, qinv);
+              a1[c] = f64_mulmod_h(ring[c][slot][jo][sl].d, k(2 * NDIG), q, qinv);
             }
           }
         } else {
@@ -322,20 +414,16 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
             double s0 = a0[c], s1 = a1[c];  // |acc| <= q/2 (+ tiny) between diagonals
 #pragma unroll
             for (int j = 0; j < NDIG; j++) {
-#ifdef GW_EXP_NOLDS  // (timing experiment: no ring reads)
-              const double yv = (double)(sl + j + c);
-#else
-              const double yv = ring[c][slot][j][sl];
-#endif
+              const double yv = ring[c][slot][j][sl].d;
               if (j == 2) {  // three digits: fold before the third product
                 s0 = f64_red(s0, q, qinv);
                 s1 = f64_red(s1, q, qinv);
               }
-              s0 += f64_mulmod_h(yv, k[j], q, qinv);
-              s1 += f64_mulmod_h(yv, k[NDIG + j], q, qinv);
+              s0 += f64_mulmod_h(yv, k(j), q, qinv);
+              s1 += f64_mulmod_h(yv, k(NDIG + j), q, qinv);
             }
             if (qs)
-              s0 += f64_mulmod_h(ring[c][slot][NDIG][sl], k[2 * NDIG], q, qinv);
+              s0 += f64_mulmod_h(ring[c][slot][NDIG][sl].d, k(2 * NDIG), q, qinv);
             a0[c] = f64_red(s0, q, qinv);  // (|s0| < 3.2 q before)
             a1[c] = f64_red(s1, q, qinv);
           }
@@ -347,13 +435,23 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       if ((unsigned)c >= nc)
         continue;
       uint64_t *op = a.acc + (size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff;
-      double s0 = a0[c], s1 = a1[c];
-      if (a.accumulate) {
-        s0 += f64_from_u52(op[0]);
-        s1 += f64_from_u52(op[apoly]);
+      if constexpr (INT) {
+        uint64_t s0 = u0[c] >= qi ? u0[c] - qi : u0[c], s1 = u1[c] >= qi ? u1[c] - qi : u1[c];
+        if (a.accumulate) {
+          s0 = add_mod(s0, op[0], qi);
+          s1 = add_mod(s1, op[apoly], qi);
+        }
+        op[0] = s0;
+        op[apoly] = s1;
+      } else {
+        double s0 = a0[c], s1 = a1[c];
+        if (a.accumulate) {
+          s0 += f64_from_u52(op[0]);
+          s1 += f64_from_u52(op[apoly]);
+        }
+        op[0] = f64_canon(s0, q, qinv);
+        op[apoly] = f64_canon(s1, q, qinv);
       }
-      op[0] = f64_canon(s0, q, qinv);
-      op[apoly] = f64_canon(s1, q, qinv);
     }
     __syncthreads();  // the ring slots the next advance overwrites were read here
   }
@@ -367,24 +465,38 @@ static GwMods gw_mods(unsigned lvl)
   GwMods md{};
   const unsigned nm = lvl + G.K;
   for (unsigned t = 0; t < nm; t++) {
-    const uint64_t qq = G.q[t < lvl ? t : G.L + (t - lvl)];
+    const unsigned m = t < lvl ? t : G.L + (t - lvl);
+    const uint64_t qq = G.q[m];
     md.q[t] = (double)qq;
     md.qinv[t] = 1.0 / (double)qq;
+    md.qi[t] = qq;
+    md.qni[t] = G.mc[m].qneg_inv;
   }
   return md;
 }
 
+// bit t: basis slot t of basis_qp(lvl) on 64-bit integer arithmetic (the
+// modulus is not below 2^51, or this ring has no FP64 twiddles): the
+// kernels' own choice (with_arith)
+static uint64_t gw_intmask(unsigned lvl)
+{
+  uint64_t mask = 0;
+  for (unsigned t = 0; t < lvl + G.K; t++)
+    if (!G.twd || G.q[t < lvl ? t : G.L + (t - lvl)] >= F64_QMAX)
+      mask |= 1ull << t;
+  return mask;
+}
+
 bool k_gemv_win_ok(unsigned lvl)
 {
-  if (G.logn < 13 || G.logn > 17 || !G.twd || G.alpha > 8)
+  if (G.logn < 13 || G.logn > 17 || G.alpha > 8)
     return false;
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
   if (ndig < 1 || ndig > 3 || nm > GPQHE_MAXMOD / 2)
     return false;
-  for (unsigned t = 0; t < nm; t++)
-    if (G.q[t < lvl ? t : G.L + (t - lvl)] >= F64_QMAX)
-      return false;
-  return true;
+  // integer slots need the split key switch's ModUp (k_modup_c1_split): the
+  // fallback conversion below is FP64 only
+  return gw_intmask(lvl) == 0 ? G.twd != nullptr : k_ks_fused_ok();
 }
 
 static uint64_t gw_pow(uint64_t b, uint64_t e, uint64_t mask)
@@ -418,6 +530,7 @@ double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
     const unsigned cnt = std::min(FoldArgs::MAX, E - e0);
     FoldArgs fa{};
     fa.e0 = e0;
+    fa.intmask = gw_intmask(lvl);
     for (unsigned e = 0; e < cnt; e++) {
       fa.pt[e] = dg[e0 + e].pt;
       fa.evk[e] = dg[e0 + e].evk;
@@ -451,6 +564,8 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
         if (!(t >= j * alpha && t < std::min(j * alpha + alpha, lvl)))
           yi[(size_t)t * 3 + j] = (int)(j * nm + t);
   } else {
+    if (gw_intmask(lvl))
+      gpqhe_die("gemv batch: no ModUp form for integer moduli at this ring");
     unsigned mods[GPQHE_MAXMOD], S = 0;
     for (unsigned j = 0; j < ndig; j++) {
       const unsigned lo = j * alpha, hi = std::min(lo + alpha, lvl);
@@ -517,7 +632,13 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   a.count = cnt;
   a.nseg = nseg;
   a.alpha = alpha;
-  const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, nm * 2 * nseg));
+  // the basis slots by arithmetic class: one launch per class and diagonal run
+  const uint64_t imask = gw_intmask(lvl);
+  GemvWin acls[2] = {a, a};  // [0] FP64 slots, [1] integer slots
+  for (unsigned t = 0; t < nm; t++) {
+    GemvWin &c = acls[(imask >> t) & 1];
+    c.slot[c.ns++] = (uint8_t)t;
+  }
   uint32_t *tab = (uint32_t *)pool_alloc((size_t)2 * P * 32 * 4);
   bool first = true;
   for (unsigned e0 = 0; e0 < E;) {
@@ -545,12 +666,28 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
       // per slot and orbit, writes (or updates) the accumulators
       ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + lvl + (first ? 2.0 : 4.0) * nm) +
                                            (double)a.E * nm * (2 * ndig + 1)));
-      switch (ndig) {
-      case 1: hipLaunchKernelGGL((gemv_win_kernel<1, 16>), grid, dim3(1024), 0, G.stream, a); break;
-      case 2: hipLaunchKernelGGL((gemv_win_kernel<2, 16>), grid, dim3(1024), 0, G.stream, a); break;
-      default: hipLaunchKernelGGL((gemv_win_kernel<3, 16>), grid, dim3(1024), 0, G.stream, a); break;
+      for (int ic = 0; ic < 2; ic++) {
+        GemvWin &c = acls[ic];
+        if (!c.ns)
+          continue;
+        memcpy(c.d, a.d, sizeof a.d);
+        memcpy(c.hm, a.hm, sizeof a.hm);
+        c.tab = a.tab;
+        c.E = a.E;
+        c.e0 = a.e0;
+        c.accumulate = a.accumulate;
+        const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, c.ns * 2 * nseg));
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, G.stream, c); };
+        switch (ndig * 2 + ic) {
+        case 2: go(gemv_win_kernel<1, 16, false>); break;
+        case 3: go(gemv_win_kernel<1, 16, true>); break;
+        case 4: go(gemv_win_kernel<2, 16, false>); break;
+        case 5: go(gemv_win_kernel<2, 16, true>); break;
+        case 6: go(gemv_win_kernel<3, 16, false>); break;
+        default: go(gemv_win_kernel<3, 16, true>); break;
+        }
+        HIP_CHECK(hipGetLastError());
       }
-      HIP_CHECK(hipGetLastError());
     }
     first = false;
     e0 = e1;

@@ -2651,18 +2651,23 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
   const ModConst mc = mcs[limb];
   const unsigned row0 = tile * T::R;
   const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
-  const uint64_t *pa = a + p * in_stride + in_pstride + off, *pb = b + p * in_stride + in_pstride + off;
+  // b null: the c1 of a ciphertext alone (the ModUp of he_gemv / he_rot
+  // batches on prime sets without the all-FP64 form, k_modup_c1_split)
+  const uint64_t *pa = a + p * in_stride + in_pstride + off, *pb = b ? b + p * in_stride + in_pstride + off : pa;
   // this thread's 8 consecutive words 8 th + k are exactly its round-C
   // elements of the inverse row pass: 16-byte loads, no transpose through LDS
   const int th = threadIdx.x, row = th / T::TA, l = th % T::TA;
   uint64_t A1[8], B1[8];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const ulonglong2 x = ((const ulonglong2 *)(pa + 8 * th))[i], z = ((const ulonglong2 *)(pb + 8 * th))[i];
+    const ulonglong2 x = ((const ulonglong2 *)(pa + 8 * th))[i];
     A1[2 * i] = x.x;
     A1[2 * i + 1] = x.y;
-    B1[2 * i] = z.x;
-    B1[2 * i + 1] = z.y;
+    if (b) {
+      const ulonglong2 z = ((const ulonglong2 *)(pb + 8 * th))[i];
+      B1[2 * i] = z.x;
+      B1[2 * i + 1] = z.y;
+    }
   }
   uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
   with_arith(mc.q, limb, logn, tw, [&](const auto &ar) {
@@ -2674,8 +2679,7 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
       if constexpr (std::is_same<A, ArF64>::value) {
         // exact FP64 product of canonical residues, |.| < 1.5 q (a valid
         // inverse-pass input); canonical only for the optional d2 copy
-        const double bb = f64_from_u52(B1[k]);
-        r[k] = f64_mulmod_h(f64_from_u52(A1[k]), bb, ar.q, ar.qinv);
+        r[k] = b ? f64_mulmod_h(f64_from_u52(A1[k]), f64_from_u52(B1[k]), ar.q, ar.qinv) : f64_from_u52(A1[k]);
         if (d2)
           raw[k] = ar.canon(r[k]);
         if (ysc) {
@@ -2685,7 +2689,7 @@ __global__ void __launch_bounds__(256) d2_rows_kernel(uint64_t *d2, uint64_t *y,
           r[k] = f64_mulmod_h(f64_red(r[k], ar.q, ar.qinv), sd, ar.q, ar.qinv);
         }
       } else {
-        raw[k] = mul_mod(A1[k], B1[k], mc);
+        raw[k] = b ? mul_mod(A1[k], B1[k], mc) : A1[k];
         r[k] = A::load(ysc ? mul_shoup(raw[k], ysc[2 * limb], ysc[2 * limb + 1], mc.q) : raw[k]);
       }
     }
@@ -2807,7 +2811,7 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
 {
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
   const unsigned n = G.n;
-  bool allf = !cols && !d2 && G.twd != nullptr && GPQHE_D2Q;
+  bool allf = !cols && !d2 && b && G.twd != nullptr && GPQHE_D2Q;
   for (unsigned i = 0; i < lvl; i++)
     allf &= G.q[i] < (1ull << 51);
   if (allf) {
@@ -2823,7 +2827,7 @@ static void d2_intt_launch(uint64_t *d2, uint64_t *ybuf, const uint64_t *a, cons
   }
   {
     // reads a1, b1; writes its inverse row pass (and d2 when asked)
-    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * (d2 ? 4 : 3));
+    ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * ((b ? 2 : 1) + 1 + (d2 ? 1 : 0)));
     hipLaunchKernelGGL((d2_rows_kernel<LOGN2>), dim3(lvl * count * (n / 2048)), dim3(256), 0, G.stream, d2, ybuf, a,
                        b, in_stride, in_pstride, G.logn, lvl, count, tw, G.dev.mc,
                        cols ? (const uint64_t *)nullptr : (const uint64_t *)tab.ysc);
@@ -3862,12 +3866,13 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
 }
 
 // ModUp of the c1 of `count` ciphertexts (he_gemv / he_rot batches,
-// gemv_win.hip) through the split key switch's first two kernels, every
-// modulus below 2^51: y = the inverse row pass of c1 x n^-1 [(Q_j/q_i)^-1]
-// (d2_rows_q_kernel<ONE>), then the column INTT, the conversion and the
-// forward column pass (ks_cols) -> T1 [count][ndig][nm][n] (own-digit slots
-// not written), then the forward row pass of every converted slot: T1 ends in
-// NTT form.  False when this ring / prime set has no such form.
+// gemv_win.hip) through the split key switch's first two kernels: y = the
+// inverse row pass of c1 x n^-1 [(Q_j/q_i)^-1] (d2_rows_q_kernel<ONE> when
+// every modulus is below 2^51, else d2_rows_kernel on c1 alone), then the
+// column INTT, the conversion and the forward column pass (ks_cols) -> T1
+// [count][ndig][nm][n] (own-digit slots not written), then the forward row
+// pass of every converted slot: T1 ends in NTT form.  False when this ring has
+// no split key switch.
 template <int LOGT1, int LOGN2>
 static bool modup_c1_launch(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, size_t x_stride, size_t x_pstride,
                             unsigned count, unsigned lvl)
@@ -3875,10 +3880,13 @@ static bool modup_c1_launch(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, siz
   const UpTable &up = up_table(lvl);
   const unsigned nm = up.nm, ndig = up.ndig, n = G.n;
   const unsigned na_min = lvl - (ndig - 1) * G.alpha;
-  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl));
-  if (!up.f64 || !invc || !GPQHE_D2Q || !G.twd)
-    return false;
-  {
+  const bool invc = G.alpha <= 4 && (nm - na_min <= 8 || ks_colsf_ok(up, lvl) ||
+                                     (!up.f64 && colsm_ks_ok<LOGT1>(nm - na_min)));
+  if (!up.f64 || !invc || !GPQHE_D2Q || !G.twd) {
+    // any other prime set (60-bit q_0 / P: the mixed-set column kernels):
+    // the relinearization's first two stages on c1 alone
+    d2_intt_launch<LOGT1, LOGN2>(nullptr, ybuf, x, nullptr, x_stride, x_pstride, count, lvl, up, !invc);
+  } else {
     const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
     ProfScope ps(KC_D2_ROWS, 8.0 * n * lvl * count * 2);
     constexpr int QN = 2;
@@ -3888,7 +3896,7 @@ static bool modup_c1_launch(uint64_t *T1, uint64_t *ybuf, const uint64_t *x, siz
                        tw, G.dev.mc, (const uint64_t *)up.ysc);
     HIP_CHECK(hipGetLastError());
   }
-  ks_cols_stage<LOGT1>(ybuf, T1, count, lvl, true);
+  ks_cols_stage<LOGT1>(ybuf, T1, count, lvl, invc);
   for (unsigned j = 0; j < ndig; j++) {
     const unsigned lo = j * G.alpha, hi = std::min(lo + G.alpha, lvl);
     for (unsigned r = 0; r < 2; r++) {  // the slots before and after the digit

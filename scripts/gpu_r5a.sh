@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-5 check run: every GPU test, smoke, the default bench without the CPU
+# leg, then the split key switch's stream-arrangement A/B (gpu_pipe_ab.sh).
+#   RUN=name [SKIP_TESTS=1] [ROUNDS=1] bash scripts/gpu_r5a.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${RUN:-r5a}
+mkdir -p $OUT
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest.log; exit 1; }
+  tail -2 $OUT/pytest.log
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; cat $OUT/smoke.log; exit 1; }
+  tail -1 $OUT/smoke.log
+fi
+timeout -k 10 600 python bench.py --no-cpu > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 1; }
+python scripts/ab_summary.py $OUT/bench.log 2>/dev/null | head -40
+RUN=${RUN:-r5a}/pipe ROUNDS=${ROUNDS:-1} bash scripts/gpu_pipe_ab.sh

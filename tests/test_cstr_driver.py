@@ -13,7 +13,8 @@ Finding (documented in DESIGN.md 5d): at N = 100 the reference's
 ctr_hempc writes n (N/10 + 1) = 33 rows into its 32 x 32 stack matrix BBz
 (src/hempc.c:233-234 -> d2z_matrix, src/matrices.c:140), corrupting a stack
 neighbour.  With the reference's own flags (-Og) the encrypted 100-step
-trajectory then leaves the plaintext one by ~0.4 % whatever the engine.
+trajectory then leaves the plaintext one by up to 1.3 % (0.37 % at steady
+state) whatever the engine.
 Built with AddressSanitizer in recover mode the stray write lands in a
 redzone, and the same unchanged caller over the oracle engine matches the
 fixture to ~3e-11.  The GPU leg (tests/test_gpu_hectr_caller.py) runs the

@@ -267,8 +267,8 @@ def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkey
     prefetch, the key tile shared by the quarters and reused across pairs,
     the accumulator restart), 17 pairs in chunks of 5/5/5/2 (the multi-chunk
     loop, a short last chunk) and the bench's own 256 pairs (one chunk of the
-    8 GiB workspace as two 128-pair sub-chunks on two streams, about 3 pairs
-    per quarter), every output residue compared with the oracle.  Also 17
+    8 GiB workspace, run as two 128-pair sub-chunks on two streams of that
+    one chunk, about 3 pairs per quarter), every output residue compared with the oracle.  Also 17
     pairs of config 5 (n=2^17, L=12,
     the three-digit split key switch), config 5's own bench shape (64 pairs per
     GPU, bench.py's c5 leg: its pair ranges and member split), both on the

@@ -5,8 +5,10 @@ HECTR's hot call is he_gemv (reference src/hempc.c:257-259) with `slots`
 rotation keys from he_genrk (src/ctr.c:521,526-532).  test_gpu_parity.py
 covers them at n <= 2^13; here they run at N=2^16, L=8 on both prime sets of
 the headline (bench51: every modulus below 2^51, the FP64 path; bench_d2: the
-60-bit q0 / P set) and at config 5's N=2^17, L=12 (c5f), with 16 slots
-(HECTR's own count) and 64:
+60-bit q0 / P set, whose q0 and P slots take the integer form of the
+inner-product kernel and the mixed-set ModUp / ModDown) and at config 5's
+N=2^17, L=12 on both (c5f, c5), with 16 slots (HECTR's own count) and 64; the
+batch entry points also at n = 2^13 / 2^15 on mixed sets (c1, hyb, c15):
 
 * he_genrk: a subset of the rotation keys, residue by residue;
 * he_rot by 1, 3 and slots - 1;
@@ -51,7 +53,7 @@ def sample_matrix(s, seed):
 
 
 @pytest.mark.parametrize("name,slots", [("bench51", 16), ("bench51", 64), ("bench_d2", 16), ("c5f", 16),
-                                        ("c5f", 64)])
+                                        ("c5f", 64), ("c5", 16)])
 def test_genrk_rot_gemv_large_n(oracle, product, name, slots):
     init_slots(oracle, product, name, slots)
     s = slots
@@ -107,8 +109,10 @@ def run_batch(oracle, product, ko, kp, fn, host_in, out_words, *args):
 
 
 @pytest.mark.parametrize("name,slots,cnt,lvl", [("bench51", 16, 3, 8), ("bench51", 16, 17, 8), ("bench51", 64, 5, 8),
-                                                ("bench51", 16, 4, 5), ("bench_d2", 16, 3, 8), ("c5f", 16, 3, 12),
-                                                ("c5f", 64, 2, 12), ("c14", 16, 9, 6)])
+                                                ("bench51", 16, 4, 5), ("bench_d2", 16, 3, 8), ("bench_d2", 16, 17, 8),
+                                                ("bench_d2", 16, 4, 5), ("c5f", 16, 3, 12), ("c5f", 64, 2, 12),
+                                                ("c5", 16, 2, 12), ("c14", 16, 9, 6), ("c15", 16, 5, 6),
+                                                ("c1", 16, 3, 4), ("hyb", 16, 3, 5)])
 def test_gemv_rot_batch(oracle, product, name, slots, cnt, lvl):
     """he_gemv_batch and he_rot_batch over `cnt` real encryptions at level
     lvl (below the top: a partial digit at lvl 5 of bench51), every output
