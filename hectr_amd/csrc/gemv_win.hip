@@ -54,14 +54,27 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 }
 
 // ---------------------------------------------------------------------------
-// Folded keys, output order, interleaved: K[(((t Etot + e) n + k) KW + w] for
-// output position k of basis slot t (KW = 2 ndig + 2, the last word padding):
+// Folded keys, output order, interleaved: slot t's block at gw_kbase(t),
+// then [(e n + k) KW_t + w] for output position k (KW_t = 2 ndig + 2 on q
+// slots, the last word padding; 2 ndig on P slots, which have no P pt word):
 //   w < ndig:           [pt_d]_t[k] [b_{d,w}]_t[k]
 //   ndig <= w < 2 ndig: [pt_d]_t[k] [a_{d,w-ndig}]_t[k]
 //   w = 2 ndig:         [P pt_d]_t[k] on q slots (t < lvl), else 0
 // pt null: 1 (a rotation).  Exact integers below 2^51 as doubles.
 // grid: (n / 256, nm, diagonals of this launch)
 // ---------------------------------------------------------------------------
+// words of one (diagonal, position) and the start of slot t's block (in
+// words, E diagonals)
+__host__ __device__ __forceinline__ unsigned gw_kw(unsigned t, unsigned lvl, unsigned ndig)
+{
+  return 2 * ndig + (t < lvl ? 2 : 0);
+}
+__host__ __device__ __forceinline__ size_t gw_kbase(unsigned t, unsigned lvl, unsigned ndig, unsigned E, unsigned logn)
+{
+  const unsigned tq = t < lvl ? t : lvl, tp = t - tq;
+  return ((size_t)tq * (2 * ndig + 2) + (size_t)tp * 2 * ndig) * E << logn;
+}
+
 struct FoldArgs {
   static constexpr unsigned MAX = 16;
   const uint64_t *pt[MAX], *evk[MAX];
@@ -78,20 +91,22 @@ __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, 
   const ModConst mc = mcs[m];
   const uint64_t *pt = fa.pt[e], *ev = fa.evk[e];
   const uint64_t w = pt ? pt[((size_t)t << logn) + k] : 1;
-  const unsigned kw = 2 * ndig + 2;
+  const unsigned kw = gw_kw(t, lvl, ndig);
   const bool isint = (fa.intmask >> t) & 1;
   // FP64 slots: the residue as a double; integer slots: its Montgomery form
   // x 2^64 mod q (bits), so the kernel's REDC of y x returns y x mod q
   auto put = [&](double *o, uint64_t v) {
     *(uint64_t *)o = isint ? mul_mod(v, mc.r64, mc) : (uint64_t)__double_as_longlong((double)v);
   };
-  double *o = K + ((((size_t)t * Etot + fa.e0 + e) << logn) + k) * kw;
+  double *o = K + gw_kbase(t, lvl, ndig, Etot, logn) + ((((size_t)fa.e0 + e) << logn) + k) * kw;
   for (unsigned j = 0; j < ndig; j++) {
     put(o + j, ev ? mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0);
     put(o + ndig + j, ev ? mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0);
   }
-  put(o + 2 * ndig, t < lvl ? mul_mod(w, mc.pmod, mc) : 0);
-  put(o + 2 * ndig + 1, 0);
+  if (t < lvl) {
+    put(o + 2 * ndig, mul_mod(w, mc.pmod, mc));
+    put(o + 2 * ndig + 1, 0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -275,7 +290,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     }
     sp[c][NDIG] = xb + ((size_t)(qs ? t : 0) << logn);
   }
-  const double *Kt = a.K + (((size_t)t * a.Etot + a.e0) << logn) * KW;
+  const unsigned kwt = qs ? KW : KW - 2;  // P slots: no P pt word, no padding
+  const double *Kt = a.K + gw_kbase(t, a.lvl, NDIG, a.Etot, logn) + ((size_t)a.e0 << logn) * kwt;
   const size_t apoly = (size_t)a.nm << logn;
   const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
   uint64_t pv[C][NWD];
@@ -330,10 +346,10 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       // next diagonal's key words in flight meanwhile
       uint64_t kc[KW], kn[KW];
       auto load_keys = [&](int e, uint64_t (&kk)[KW]) {
-        const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
+        const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * kwt);
 #pragma unroll
         for (int w = 0; w < KW / 2; w++) {
-          const ulonglong2 v = kp[w];
+          const ulonglong2 v = (w < NDIG || qs) ? kp[w] : make_ulonglong2(0, 0);
           kk[2 * w] = v.x;
           kk[2 * w + 1] = v.y;
         }
@@ -379,10 +395,14 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     constexpr int KD = 3;
     uint64_t kw[KD][KW];
     auto load_keys = [&](int e) {
-      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
+#ifdef GW_EXP_NOKEY  // (timing experiment: every diagonal takes diagonal 0's keys)
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + koff * kwt);
+#else
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * kwt);
+#endif
 #pragma unroll
       for (int w = 0; w < KW / 2; w++) {
-        const ulonglong2 v = kp[w];
+        const ulonglong2 v = (w < NDIG || qs) ? kp[w] : make_ulonglong2(0, 0);
         kw[e % KD][2 * w] = v.x;
         kw[e % KD][2 * w + 1] = v.y;
       }
@@ -414,7 +434,11 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
             double s0 = a0[c], s1 = a1[c];  // |acc| <= q/2 (+ tiny) between diagonals
 #pragma unroll
             for (int j = 0; j < NDIG; j++) {
+#ifdef GW_EXP_NOLDS  // (timing experiment: no ring reads)
+              const double yv = (double)(sl + j + c);
+#else
               const double yv = ring[c][slot][j][sl].d;
+#endif
               if (j == 2) {  // three digits: fold before the third product
                 s0 = f64_red(s0, q, qinv);
                 s1 = f64_red(s1, q, qinv);
@@ -519,7 +543,7 @@ static void gw_galois(unsigned d, uint64_t &g, uint64_t &gi)
 size_t k_gemv_fold_words(unsigned E, unsigned lvl)
 {
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
-  return (size_t)nm * E * (2 * ndig + 2) * G.n;
+  return gw_kbase(nm, lvl, ndig, E, G.logn);
 }
 
 double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)

@@ -353,10 +353,24 @@ __global__ void __launch_bounds__(256 * QN, 1)
             for (int k = 0; k < 8; k++)
               o[k] = sub_mod(half ? a1[k] : a0[k], ar.canon(r[k]), q);
           }
-          ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + 8 * th);
+          // The wave's 64 threads hold its 4 KiB of consecutive words, 64 B
+          // each: transposed through the wave's own rows of the LDS tile
+          // (free again after the row pass) so that each 16-byte store
+          // instruction writes 1 KiB contiguous (consecutive lanes 16 B
+          // apart).  Lanes 64 B apart store at ~4.2 TB/s against ~5.6 for
+          // that shape (copy kernels, scripts/ubench_lanes.hip): keep 1839 -
+          // 1853 -> 1798 - 1814 us per chunk, same box.
+          const int e0 = (th & ~63) * 8, ln = th & 63;
+          ulonglong2 *wr = (ulonglong2 *)(lq + (e0 >> LOGN2) * T::RS);
+          wave_sync();  // the row pass's last reads of these words
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            wr[4 * ln + i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
+          wave_sync();
+          ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + e0);
 #pragma unroll
           for (int i = 0; i < 4; i++)  // (non-temporal stores here: 1840 -> 2245 us per chunk)
-            d2[i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
+            d2[64 * i + ln] = wr[64 * i + ln];
         }
       } else {
 #pragma unroll
