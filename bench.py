@@ -760,6 +760,14 @@ def gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
                 "rot_batch": {"value": vra, "unit": "rotations/s", "us_per_rotation_per_gpu": 1e6 * world / vra},
                 "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0], "us_per_gemv": w[1] / (steps * B)}
                             for k, w in sorted(sta.items(), key=lambda kv: -kv[1][1])}}
+            try:
+                gd = json.load(open(os.path.join(ROOT, "profiles", "r5_gemv_baseline_generic_d2.json")))
+                leg["alt_primes"]["generic_path_us_per_gemv"] = gd["gemv_batch_us_per_ct"]
+                leg["alt_primes"]["generic_path_source"] = ("profiles/r5_gemv_baseline_generic_d2.json (round-4 "
+                                                            "kernels, same shape)")
+                leg["alt_primes"]["speedup_vs_generic"] = gd["gemv_batch_us_per_ct"] / (1e6 * world / va)
+            except (OSError, ValueError, KeyError):
+                pass
         ga.close()
         barrier()
     if args.check_shards:

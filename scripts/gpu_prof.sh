@@ -28,3 +28,5 @@ pass hit --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
 pass sq --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE || exit 1
 # the VALU instruction mix: FP64 classes (v_rndne_f64 counts in none of them), integer, conversions
 pass f64 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU || exit 1
+# the gemv leg's kernels (he_gemv_batch at the bench shape, 256 ciphertexts)
+timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/gemv_kt -o gemv_kt --output-format csv -- python scripts/gemv_time.py --set bench51 --count 256 --single 0 > $OUT/gemv_kt.log 2>&1 || exit 1
