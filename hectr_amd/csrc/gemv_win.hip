@@ -251,6 +251,12 @@ __device__ __forceinline__ void gw_mac128(uint64_t &hi, uint64_t &lo, uint64_t y
 // forms (gemv_fold_kernel), a diagonal's products are summed in 128 bits
 // (at most 2 ndig + 1 < 2^4 products of residues below q < 2^60: below
 // q 2^64) and reduced by one REDC, the accumulators kept in [0, 2q).
+// LZ (FP64 slots with q < 2^50, at most two digits; chosen per workgroup
+// around the advance loop): the accumulators are reduced every third diagonal
+// instead of every one.  With centred ring values
+// |y| <= q/2 < 2^49 a product is below q (1/2 + 1.5 |y| 2^-52) < 0.69 q, so
+// three diagonals of three products on top of |acc| <= q/2 stay below 6.9 q
+// < 2^52.8 (and one more canonical word added at the output below 2^53).
 template <int NDIG, int W, bool INT>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
@@ -316,6 +322,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       }
   };
   const unsigned nadv = SEG / 16;
+  auto advances = [&](auto lzc) {
+  constexpr bool LZ = decltype(lzc)::value;
   for (unsigned adv = 0; adv < nadv; adv++) {
     const unsigned ob = o0 + adv * 16;
     if (adv == 0) {
@@ -448,8 +456,13 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
             }
             if (qs)
               s0 += f64_mulmod_h(ring[c][slot][NDIG][sl].d, k(2 * NDIG), q, qinv);
-            a0[c] = f64_red(s0, q, qinv);  // (|s0| < 3.2 q before)
-            a1[c] = f64_red(s1, q, qinv);
+            if (!LZ || NDIG > 2 || e % 3 == 2) {
+              a0[c] = f64_red(s0, q, qinv);  // (|s0| < 3.2 q before; LZ: < 6.9 q)
+              a1[c] = f64_red(s1, q, qinv);
+            } else {
+              a0[c] = s0;
+              a1[c] = s1;
+            }
           }
         }
       }
@@ -479,6 +492,11 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     }
     __syncthreads();  // the ring slots the next advance overwrites were read here
   }
+  };
+  if (!INT && NDIG <= 2 && q < (double)F64_LAZY)
+    advances(std::true_type{});
+  else
+    advances(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------
