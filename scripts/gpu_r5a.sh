@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 check run: every GPU test, smoke, the default bench without the CPU
-# leg, then the split key switch's stream-arrangement A/B (gpu_pipe_ab.sh).
+# leg.
 #   RUN=name [SKIP_TESTS=1] [ROUNDS=1] bash scripts/gpu_r5a.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -15,4 +15,3 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 600 python bench.py --no-cpu > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 1; }
 python scripts/ab_summary.py $OUT/bench.log 2>/dev/null | head -40
-RUN=${RUN:-r5a}/pipe ROUNDS=${ROUNDS:-1} bash scripts/gpu_pipe_ab.sh
