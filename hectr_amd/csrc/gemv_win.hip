@@ -80,7 +80,15 @@ struct FoldArgs {
   const uint64_t *pt[MAX], *evk[MAX];
   unsigned e0;       // the launch's first diagonal in K
   uint64_t intmask;  // bit t: basis slot t on 64-bit integer arithmetic (modulus >= 2^51)
+  unsigned split;    // integer slots' moduli all below 2^60: words stored as 30-bit halves (gw_split)
 };
+
+// x < 2^60 as its 30-bit halves in the two 32-bit words (x0 | x1 << 32), the
+// operands of v_mad_u64_u32
+__host__ __device__ __forceinline__ uint64_t gw_split(uint64_t x)
+{
+  return (x & ((1ull << 30) - 1)) | ((x >> 30) << 32);
+}
 
 __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, unsigned Etot, unsigned ndig,
                                                         unsigned logn, unsigned lvl, unsigned L, unsigned nmod,
@@ -96,7 +104,12 @@ __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, 
   // FP64 slots: the residue as a double; integer slots: its Montgomery form
   // x 2^64 mod q (bits), so the kernel's REDC of y x returns y x mod q
   auto put = [&](double *o, uint64_t v) {
-    *(uint64_t *)o = isint ? mul_mod(v, mc.r64, mc) : (uint64_t)__double_as_longlong((double)v);
+    if (isint) {
+      const uint64_t m = mul_mod(v, mc.r64, mc);
+      *(uint64_t *)o = fa.split ? gw_split(m) : m;
+    } else {
+      *(uint64_t *)o = (uint64_t)__double_as_longlong((double)v);
+    }
   };
   double *o = K + gw_kbase(t, lvl, ndig, Etot, logn) + ((((size_t)fa.e0 + e) << logn) + k) * kw;
   for (unsigned j = 0; j < ndig; j++) {
@@ -246,6 +259,34 @@ __device__ __forceinline__ void gw_mac128(uint64_t &hi, uint64_t &lo, uint64_t y
   hi += ph + (lo < pl);
 }
 
+// the split form (moduli below 2^60, operands gw_split): y w as four 32 x 32
+// products of 30-bit halves into three 64-bit sums -- s00 += y0 w0, s01 +=
+// y0 w1 + y1 w0, s11 += y1 w1 -- each term below 2^60, so up to 2^3 products'
+// sums stay below 2^63 with no carries: four v_mad_u64_u32 per product
+// instead of a 64 x 64 -> 128-bit product (about eight multiplies and the
+// carries)
+struct GwAcc3 {
+  uint64_t s00 = 0, s01 = 0, s11 = 0;
+  __device__ __forceinline__ void mac(uint64_t y, uint64_t w)
+  {
+    const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+    s00 += (uint64_t)y0 * w0;
+    s01 += (uint64_t)y0 * w1;
+    s01 += (uint64_t)y1 * w0;
+    s11 += (uint64_t)y1 * w1;
+  }
+  // REDC of s00 + s01 2^30 + s11 2^60 (< q 2^64): [0, 2q)
+  __device__ __forceinline__ uint64_t redc(uint64_t q, uint64_t qni) const
+  {
+    uint64_t lo = s00 + (s01 << 30);
+    uint64_t hi = (s01 >> 34) + (lo < s00);
+    const uint64_t u = s11 << 60;
+    lo += u;
+    hi += (s11 >> 4) + (lo < u);
+    return gw_redc(hi, lo, q, qni);
+  }
+};
+
 // INT: the slots of this launch are on 64-bit integer moduli (q >= 2^51: the
 // 60-bit q_0 / P of HECTR-like prime sets).  Their key words are Montgomery
 // forms (gemv_fold_kernel), a diagonal's products are summed in 128 bits
@@ -257,7 +298,7 @@ __device__ __forceinline__ void gw_mac128(uint64_t &hi, uint64_t &lo, uint64_t y
 // |y| <= q/2 < 2^49 a product is below q (1/2 + 1.5 |y| 2^-52) < 0.69 q, so
 // three diagonals of three products on top of |acc| <= q/2 stay below 6.9 q
 // < 2^52.8 (and one more canonical word added at the output below 2^53).
-template <int NDIG, int W, bool INT>
+template <int NDIG, int W, bool INT, bool SPLIT = false>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
   constexpr int C = gw_cts<NDIG>(), RING = 32, NWD = NDIG + 1, KW = 2 * NDIG + 2;
@@ -316,7 +357,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 #pragma unroll
       for (int w = 0; w < NWD; w++) {
         if constexpr (INT)
-          ring[c][slot][w][L].u = pv[c][w];
+          ring[c][slot][w][L].u = SPLIT ? gw_split(pv[c][w]) : pv[c][w];
         else
           ring[c][slot][w][L].d = gw_center(f64_from_u52(pv[c][w]), q);
       }
@@ -376,9 +417,34 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 #pragma unroll
             for (int c = 0; c < C; c++) {
               const uint64_t y0 = ring[c][slot][NDIG][sl].u, y1 = ring[c][slot][jo][sl].u;
-              u0[c] = gw_redc(mulhi64(y0, kc[2 * NDIG]), y0 * kc[2 * NDIG], qi, qni);
-              u1[c] = gw_redc(mulhi64(y1, kc[2 * NDIG]), y1 * kc[2 * NDIG], qi, qni);
+              if constexpr (SPLIT) {
+                GwAcc3 b0, b1;
+                b0.mac(y0, kc[2 * NDIG]);
+                b1.mac(y1, kc[2 * NDIG]);
+                u0[c] = b0.redc(qi, qni);
+                u1[c] = b1.redc(qi, qni);
+              } else {
+                u0[c] = gw_redc(mulhi64(y0, kc[2 * NDIG]), y0 * kc[2 * NDIG], qi, qni);
+                u1[c] = gw_redc(mulhi64(y1, kc[2 * NDIG]), y1 * kc[2 * NDIG], qi, qni);
+              }
             }
+          }
+          continue;
+        }
+        if constexpr (SPLIT) {
+#pragma unroll
+          for (int c = 0; c < C; c++) {
+            GwAcc3 b0, b1;
+#pragma unroll
+            for (int j = 0; j < NDIG; j++) {
+              const uint64_t yv = ring[c][slot][j][sl].u;
+              b0.mac(yv, kc[j]);
+              b1.mac(yv, kc[NDIG + j]);
+            }
+            if (qs)
+              b0.mac(ring[c][slot][NDIG][sl].u, kc[2 * NDIG]);
+            u0[c] = lazy_lt2q(u0[c] + b0.redc(qi, qni), q2);
+            u1[c] = lazy_lt2q(u1[c] + b1.redc(qi, qni), q2);
           }
           continue;
         }
@@ -529,6 +595,15 @@ static uint64_t gw_intmask(unsigned lvl)
   return mask;
 }
 
+// the integer slots' split form (GwAcc3) applies: every integer modulus below 2^60
+static bool gw_split_ok(unsigned lvl)
+{
+  for (unsigned t = 0; t < lvl + G.K; t++)
+    if (((gw_intmask(lvl) >> t) & 1) && G.q[t < lvl ? t : G.L + (t - lvl)] >= (1ull << 60))
+      return false;
+  return true;
+}
+
 bool k_gemv_win_ok(unsigned lvl)
 {
   if (G.logn < 13 || G.logn > 17 || G.alpha > 8)
@@ -573,6 +648,7 @@ double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
     FoldArgs fa{};
     fa.e0 = e0;
     fa.intmask = gw_intmask(lvl);
+    fa.split = gw_split_ok(lvl);
     for (unsigned e = 0; e < cnt; e++) {
       fa.pt[e] = dg[e0 + e].pt;
       fa.evk[e] = dg[e0 + e].evk;
@@ -720,13 +796,14 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
         c.accumulate = a.accumulate;
         const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, c.ns * 2 * nseg));
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, G.stream, c); };
+        const bool split = gw_split_ok(lvl);
         switch (ndig * 2 + ic) {
         case 2: go(gemv_win_kernel<1, 16, false>); break;
-        case 3: go(gemv_win_kernel<1, 16, true>); break;
+        case 3: split ? go(gemv_win_kernel<1, 16, true, true>) : go(gemv_win_kernel<1, 16, true>); break;
         case 4: go(gemv_win_kernel<2, 16, false>); break;
-        case 5: go(gemv_win_kernel<2, 16, true>); break;
+        case 5: split ? go(gemv_win_kernel<2, 16, true, true>) : go(gemv_win_kernel<2, 16, true>); break;
         case 6: go(gemv_win_kernel<3, 16, false>); break;
-        default: go(gemv_win_kernel<3, 16, true>); break;
+        default: split ? go(gemv_win_kernel<3, 16, true, true>) : go(gemv_win_kernel<3, 16, true>); break;
         }
         HIP_CHECK(hipGetLastError());
       }
