@@ -627,6 +627,19 @@ def mul_ref(stream, logn, L, dnum, q0_bits, p_bits, nspecial, seed):
     return run
 
 
+def gemv_pmc():
+    """Newest committed gemv-leg PMC summary (profiles/r<round>_v<version>_gemv_pmc.json)."""
+    def order(f):
+        m = re.search(r"r(\d+)_v(\d+)_gemv_pmc", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemv_pmc.json")), key=order, reverse=True):
+        try:
+            return json.load(open(f)), os.path.relpath(f, ROOT)
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def gemv_cpu_baseline(args, slots):
     """The oracle's he_gemv_batch (CPU restatement, OpenMP over the batch: one
     ciphertext per thread) on a bounded sample of the same workload."""
@@ -730,6 +743,19 @@ def gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
                                "streamed_GBs": w[2] / w[1] / 1e3}
                            for k, w in sorted(stats.items(), key=lambda kv: -kv[1][1])},
                "data": "synthetic random-residue ciphertexts (splitmix64), real rotation keys (he_genrk)"}
+        gp = gemv_pmc()
+        if gp:
+            e = next((v for k, v in gp[0].get("kernels", {}).items() if k.startswith(dom)), None)
+            if e and "hbm_bytes" in e:
+                # the inner-product kernel's PMC passes (profiles/*_gemv_pmc.json: the
+                # same batch through scripts/gemv_time.py): HBM bytes per launch and
+                # its VALU issue fraction (it sits on neither roof: keys from L2)
+                leg["roofline"].update({"traffic": e["hbm_bytes"], "traffic_source": gp[1],
+                                        "pmc_hbm_frac": e["hbm_bytes"] / e["mean_us"] / 1e3 / HBM_PEAK_GBS,
+                                        "pmc_mean_us": e["mean_us"]})
+                for k in ("valu_frac", "valu_busy", "l2_hit_rate", "sq_wait_any"):
+                    if k in e:
+                        leg["roofline"]["pmc_" + k] = e[k]
         if generic:
             leg["generic_path_us_per_gemv"] = generic.get("gemv_batch_us_per_ct")
             leg["generic_path_source"] = "profiles/r5_gemv_baseline_generic.json (round-4 kernels, same shape)"

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--count", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--single", type=int, default=1)
+    ap.add_argument("--rot", type=int, default=1, help="0: he_gemv_batch only (profiling passes of the gemv leg)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -58,12 +59,15 @@ def main():
 
     t = timed(lambda: e.lib.he_gemv_batch(y.data_ptr(), M.ctypes.data, x.data_ptr(), cnt, L, rk))
     out["gemv_batch_us_per_ct"] = t / cnt * 1e6
-    t = timed(lambda: e.lib.he_rot_batch(r.data_ptr(), x.data_ptr(), cnt, L, 1, rk))
-    out["rot_batch_us_per_ct"] = t / cnt * 1e6
+    if args.rot:
+        t = timed(lambda: e.lib.he_rot_batch(r.data_ptr(), x.data_ptr(), cnt, L, 1, rk))
+        out["rot_batch_us_per_ct"] = t / cnt * 1e6
     # per-kernel device time of one batch of each (HIP events on the engine stream)
     for name, fn in (("gemv_batch", lambda: e.lib.he_gemv_batch(y.data_ptr(), M.ctypes.data, x.data_ptr(), cnt, L,
                                                                  rk)),
                      ("rot_batch", lambda: e.lib.he_rot_batch(r.data_ptr(), x.data_ptr(), cnt, L, 1, rk))):
+        if name == "rot_batch" and not args.rot:
+            continue
         e.prof_enable(True)
         fn()
         e.sync()

@@ -15,11 +15,14 @@ fi
 BK="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr --no-ntt --no-c5 --no-gemv --alt-bits 0 --streams 1"
 B="python bench.py --steps 3 --warmup 1 --no-cpu --no-cstr --no-ntt --no-c5 --no-gemv --alt-bits 0 --streams 1"
 N="python scripts/prof_ntt.py 1024"
-pass() {  # pass <dir> <rocprofv3 args...>  (on the bench command, then on the NTT leg)
+# the gemv leg's workload (he_gemv_batch at the bench shape, 256 ciphertexts)
+GV="python scripts/gemv_time.py --set bench51 --count 256 --single 0 --rot 0"
+pass() {  # pass <dir> <rocprofv3 args...>  (on the bench command, the NTT leg, the gemv leg)
   d=$1; shift
   cmd=$B; [ "$d" = kt ] && cmd=$BK
   timeout -s KILL 240 rocprofv3 "$@" -d $OUT/$d -o $d --output-format csv -- $cmd > $OUT/$d.log 2>&1 || return 1
   timeout -s KILL 240 rocprofv3 "$@" -d $OUT/ntt_$d -o ntt_$d --output-format csv -- $N > $OUT/ntt_$d.log 2>&1 || return 1
+  timeout -s KILL 240 rocprofv3 "$@" -d $OUT/gemv_$d -o gemv_$d --output-format csv -- $GV > $OUT/gemv_$d.log 2>&1 || return 1
 }
 pass kt --kernel-trace --stats || exit 1
 pass fetch --pmc FETCH_SIZE || exit 1
@@ -28,5 +31,3 @@ pass hit --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
 pass sq --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE || exit 1
 # the VALU instruction mix: FP64 classes (v_rndne_f64 counts in none of them), integer, conversions
 pass f64 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU || exit 1
-# the gemv leg's kernels (he_gemv_batch at the bench shape, 256 ciphertexts)
-timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/gemv_kt -o gemv_kt --output-format csv -- python scripts/gemv_time.py --set bench51 --count 256 --single 0 > $OUT/gemv_kt.log 2>&1 || exit 1

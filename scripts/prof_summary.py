@@ -8,6 +8,7 @@ writes
   <tag>_pmc.json              per kernel of the bench run: launches, mean duration, HBM bytes per
                               launch, L2 hit rate, SQ wait / VALU fractions
   <tag>_ntt_pmc.json          the same for the NTT leg
+  <tag>_gemv_kernel_stats.csv, <tag>_gemv_pmc.json  the same for the gemv leg (scripts/gemv_time.py)
   <tag>_bench.json            the default bench line of the same run (when present)
 
 Units and corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and
@@ -103,7 +104,7 @@ def main(run, tag):
             json.dump(b, open(tag + "_bench.json", "w"), indent=1)
             meta["bench_workload"] = b["config"]["workload"]
             meta["pairs_per_launch"] = b["config"].get("pairs_per_launch")
-    for prefix, suffix in (("", ""), ("ntt_", "_ntt")):
+    for prefix, suffix in (("", ""), ("ntt_", "_ntt"), ("gemv_", "_gemv")):
         if not os.path.exists(os.path.join(run, prefix + "kt")):
             continue
         shutil.copy(os.path.join(run, prefix + "kt", prefix + "kt_kernel_stats.csv"), tag + suffix + "_kernel_stats.csv")
@@ -111,7 +112,12 @@ def main(run, tag):
         m = dict(meta)
         if prefix:
             m = {k: v for k, v in meta.items() if k not in ("bench_workload", "pairs_per_launch")}
-            m["workload"] = "config 2: NTT -> INTT of 1024 polys, N=2^16, L=8 (scripts/prof_ntt.py)"
+            m["workload"] = ("config 2: NTT -> INTT of 1024 polys, N=2^16, L=8 (scripts/prof_ntt.py)" if prefix == "ntt_"
+                             else "he_gemv_batch of 256 ciphertexts, N=2^16, L=8, 16 slots, bench51 primes "
+                                  "(scripts/gemv_time.py --count 256 --rot 0; the bench's gemv leg)")
+            if prefix == "gemv_":
+                m["cts_per_launch"] = 256
+                m["mean_us"] = "kernel trace of the same command"
         json.dump({"meta": m, "kernels": out}, open(tag + suffix + "_pmc.json", "w"), indent=1)
         print(f"== {tag}{suffix}")
         for k, e in list(out.items())[:14]:
