@@ -55,3 +55,23 @@ def test_bench_two_ranks_c5_and_gemv_shards_bit_exact():
     assert c5["shard_check"] == {"pairs": 6, "ranks": 2, "bit_exact": True, "differing_pairs": []}, c5["shard_check"]
     assert g["shard_check"] == {"cts": 6, "ranks": 2, "bit_exact": True, "differing_cts": []}, g["shard_check"]
     assert len(c5["rank_times_s"]) == 2 and len(g["rank_times_s"]) == 2
+
+
+def test_bench_two_ranks_default_legs():
+    """The driver's N > 1 command shape with every leg bench.py runs there at
+    its defaults (the 60-bit alternates of the headline, config 5 and the gemv
+    leg included; NTT, CSTR and the CPU baseline are N = 1 only), small
+    batches: one JSON line carrying each leg's value and both ranks' times."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
+           "1", "--c5-batch", "2", "--gemv-batch", "3"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["value_60bit"] > 0
+    assert d["config5"]["value"] > 0 and d["config5"]["value_60bit"] > 0
+    g = d["gemv"]
+    assert g["value"] > 0 and g["alt_primes"]["value"] > 0 and len(g["rank_times_s"]) == 2
