@@ -937,12 +937,22 @@ def main():
         alt = MulBatch(stream, logn, L, dnum, args.alt_bits, args.alt_bits, 0, B, rank * B, KEY_SEED)
         alt.eng.lib.gpqhe_set_streams(args.streams)
         t = hdist.max_over_ranks(timed(alt.step, args.steps, 1, alt.eng.sync, barrier), device=red_dev)
+        alt.eng.lib.gpqhe_set_streams(1)  # instrumented single-stream pass, as the headline's
+        alt.eng.prof_enable(True)
+        for _ in range(args.steps):
+            alt.step()
+        alt.eng.sync()
+        sta = alt.eng.prof_collect()
+        alt.eng.prof_enable(False)
         if rank == 0:
             v = world * B * args.steps / t
             result["value_60bit"] = v
             result["alt_primes"] = {"q0_bits": args.alt_bits, "qi_bits": 50, "p_bits": args.alt_bits,
                                     "nspecial": alt.K, "value": v, "unit": "ct-mult/s", "steps": args.steps,
-                                    "op_roofline_frac": alt.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
+                                    "op_roofline_frac": alt.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS,
+                                    "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0],
+                                                    "us_per_pair": w[1] / (args.steps * B)}
+                                                for k, w in sorted(sta.items(), key=lambda kv: -kv[1][1])}}
         alt.close()
         barrier()
 
@@ -958,6 +968,15 @@ def main():
             c5.eng.lib.gpqhe_set_streams(args.streams)
             t_all = hdist.all_values(timed(c5.step, steps5, 1, c5.eng.sync, barrier), device=red_dev)
             t = max(t_all)
+            # instrumented single-stream pass, as the headline's: per-kernel time
+            c5.eng.lib.gpqhe_set_streams(1)
+            c5.eng.prof_enable(True)
+            for _ in range(steps5):
+                c5.step()
+            c5.eng.sync()
+            st5 = c5.eng.prof_collect()
+            c5.eng.prof_enable(False)
+            c5.eng.lib.gpqhe_set_streams(args.streams)
             leg = None
             if rank == 0:
                 v = world * args.c5_batch * steps5 / t
@@ -966,7 +985,10 @@ def main():
                        "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "ct-mult/s",
                        "steps": steps5, "ms_per_step": 1e3 * t / steps5, "rank_times_s": t_all,
                        "rank_time_min_s": min(t_all), "rank_time_max_s": t,
-                       "op_roofline_frac": c5.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS}
+                       "op_roofline_frac": c5.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS,
+                       "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0], "us_per_pair": w[1] / (steps5 * args.c5_batch),
+                                       "streamed_GBs": w[2] / w[1] / 1e3}
+                                   for k, w in sorted(st5.items(), key=lambda kv: -kv[1][1])}}
             out5 = c5.out.cpu() if args.check_shards else None
             c5.close()
             barrier()

@@ -35,6 +35,7 @@
 #include "ntt_device.h"
 #include "tables.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -850,7 +851,9 @@ void k_gemv_batch_ex(uint64_t *y, size_t y_stride, size_t y_pstride, const uint6
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
   const size_t per_ct = ((size_t)lvl + (size_t)ndig * nm + 2 * (size_t)nm) * G.n * 8;
   const size_t budget = (size_t)8 << 30;
-  const size_t chunk = std::max<size_t>(1, std::min<size_t>(budget / per_ct, 65535 / (3 * nm)));
+  size_t chunk = std::max<size_t>(1, std::min<size_t>(budget / per_ct, 65535 / (3 * nm)));
+  if (const char *e = getenv("GPQHE_GEMV_CHUNK"))  // test hook: several chunks on a small batch
+    chunk = std::max<size_t>(1, std::min<size_t>(chunk, strtoul(e, nullptr, 0)));
   for (size_t c0 = 0; c0 < count; c0 += chunk) {
     const unsigned cnt = (unsigned)std::min(chunk, count - c0);
     gemv_chunk(y + c0 * y_stride, y_stride, y_pstride, x + c0 * x_stride, x_stride, x_pstride, cnt, lvl, K, d, E,

@@ -146,3 +146,32 @@ def test_gemv_rot_batch(oracle, product, name, slots, cnt, lvl):
         assert np.abs(dz - np.roll(zs[cnt - 1], -r)).max() < 1e-6
     for e, k in ((oracle, ko), (product, kp)):
         e.free_evks(k[2])
+
+
+def test_gemv_rot_batch_chunks_and_empty(oracle, product, monkeypatch):
+    """The batch path's chunk loop (GPQHE_GEMV_CHUNK=2: 5 ciphertexts as
+    2 + 2 + 1, the workspace and orbit table per chunk) against the oracle, and
+    empty batches (count 0) that leave the output untouched."""
+    import torch
+    init_slots(oracle, product, "bench51", 16, seed=41)
+    s, n, lvl, cnt = 16, product.n, 8, 5
+    ko, kp = rot_keys(oracle), rot_keys(product)
+    rng = np.random.default_rng(5)
+    zs = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
+    Mc = np.ascontiguousarray(sample_matrix(s, 3).ravel(), dtype=np.complex128)
+    host = encrypt_batch(product, kp[0], zs, nlimbs=lvl)
+    monkeypatch.setenv("GPQHE_GEMV_CHUNK", "2")
+    want, got = run_batch(oracle, product, ko[2], kp[2], "he_gemv_batch", host, cnt * 2 * (lvl - 1) * n,
+                          Mc.ctypes.data, "IN", cnt, lvl)
+    assert np.array_equal(got, want), f"gemv: {np.count_nonzero(got != want)} residues differ"
+    want, got = run_batch(oracle, product, ko[2], kp[2], "he_rot_batch", host, cnt * 2 * lvl * n, "IN", cnt, lvl, 3)
+    assert np.array_equal(got, want), f"rot: {np.count_nonzero(got != want)} residues differ"
+    din = torch.from_numpy(host.view(np.int64)).cuda()
+    dout = torch.full((2 * lvl * n,), 7, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    product.lib.he_gemv_batch(dout.data_ptr(), Mc.ctypes.data, din.data_ptr(), 0, lvl, kp[2])
+    product.lib.he_rot_batch(dout.data_ptr(), din.data_ptr(), 0, lvl, 3, kp[2])
+    product.sync()
+    assert bool((dout == 7).all())
+    for e, k in ((oracle, ko), (product, kp)):
+        e.free_evks(k[2])
