@@ -49,6 +49,35 @@ __global__ void __launch_bounds__(256) cp(const ulonglong2 *__restrict__ in, ulo
   }
 }
 
+// keep-like mix: four input streams read per chunk (read shape R), one
+// output stream written coalesced (lanes 16 B apart)
+template <int R>
+__global__ void __launch_bounds__(256) mix(const ulonglong2 *__restrict__ in, ulonglong2 *__restrict__ o, size_t chunks)
+{
+  const unsigned t = threadIdx.x;
+  for (size_t c = blockIdx.x; c < chunks; c += gridDim.x) {
+    ulonglong2 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      acc[j] = make_ulonglong2(0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const ulonglong2 *b = in + ((size_t)s * chunks + c) * 1024;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const size_t i = R == 0 ? 256 * j + t : 4 * t + j;
+        const ulonglong2 v = b[i];
+        acc[j].x ^= v.x;
+        acc[j].y += v.y;
+      }
+    }
+    ulonglong2 *d = o + c * 1024;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      d[256 * j + t] = acc[j];
+  }
+}
+
 int main()
 {
   const size_t bytes = (size_t)2 << 30, chunks = bytes / 16384;
@@ -88,6 +117,26 @@ int main()
         if (rep)
           printf("grid %5d  %-32s read %.2f TB/s   copy %.2f TB/s (read + write)\n", grid, names[m],
                  5.0 * bytes / ms / 1e9, 5.0 * bytes / ms2 / 1e9);
+      }
+    }
+  }
+  // the mix: 4 reads + 1 write per 16 KiB chunk
+  {
+    const size_t mchunks = bytes / 16384 / 4;  // 4 input streams of mchunks chunks in a
+    for (int r = 0; r < 2; r++) {
+      for (int rep = 0; rep < 2; rep++) {
+        hipEventRecord(e0);
+        for (int i = 0; i < 5; i++) {
+          if (r == 0) hipLaunchKernelGGL(mix<0>, dim3(8192), dim3(256), 0, 0, a, b, mchunks);
+          else hipLaunchKernelGGL(mix<1>, dim3(8192), dim3(256), 0, 0, a, b, mchunks);
+        }
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (rep)
+          printf("mix 4 reads (%s) + 1 coalesced write: %.2f TB/s\n", r ? "lane-own 64 B" : "lanes 16 B apart",
+                 5.0 * (5.0 / 4.0) * bytes / ms / 1e9);
       }
     }
   }
