@@ -46,6 +46,9 @@ PARAMS = {
     # rows) and n=2^15 (128 x 256 columns, 256-element rows)
     "c14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
     "c15": ("params", dict(logn=15, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=60, qi_bits=48, p_bits=60)),
+    # 61-bit q0 / P: integer moduli of 2^60 and above (the gemv's integer form
+    # without its 30-bit-half products)
+    "i14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=61, qi_bits=48, p_bits=61)),
     # all-FP64 sets at n=2^13 and 2^15: the FP64 column kernels
     # ks_colsf<6, 8> / dn_colsf<6, .> / ntt2_colsf<6, .> (T = 64) and the
     # n=2^15 split-key-switch forms on every-modulus-below-2^51 primes
