@@ -1,11 +1,16 @@
 // gemv_win.hip - HECTR's he_gemv (reference src/hempc.c:257-259) and he_rot
-// over a batch of independent ciphertexts at n = 2^13 .. 2^17, every modulus
-// below 2^51 (FP64 arithmetic, ntt_device.h):
+// over a batch of independent ciphertexts at n = 2^13 .. 2^17 (he_gemv_batch /
+// he_rot_batch, and he_gemv / he_rot on one object at those sizes):
 //
-//   y   = INTT(c1) x [(Q_j/q_i)^-1]                 k_ntt_ex, scale folded in
-//   Dc  = NTT(FBC(y)) on every slot outside a digit  gemv_fbc_kernel + k_ntt
-//   acc = sum_d pt_d sigma_d(KS_d(c0, c1))          gemv_win_kernel (basis QP)
-//   out = ModDown(acc) by P q_top (gemv) or P (rot) k_moddown
+//   ModUp  Dc = NTT(FBC(INTT(c1) x [(Q_j/q_i)^-1]))  k_modup_c1_split: the split
+//          on every slot outside a digit             key switch's d2_rows (c1
+//                                                    form) + ks_cols + row pass
+//   acc = sum_d pt_d sigma_d(KS_d(c0, c1))           gemv_win_kernel (basis QP)
+//   out = ModDown(acc) by P q_top (gemv) or P (rot)  k_moddown_fused
+//
+// Basis slots on moduli below 2^51 run the inner products in FP64 (exact
+// products, ntt_device.h); wider ones (HECTR-like 59-61-bit q0 / P) in 64-bit
+// integers with Montgomery-form keys (gemv_win_kernel<., ., INT>).
 //
 // The oracle's hoisted gemv (oracle/ckks_oracle.c gemv_apply): one ModUp per
 // ciphertext, the rotated inner products accumulated in the extended basis,
@@ -61,7 +66,9 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 //   w < ndig:           [pt_d]_t[k] [b_{d,w}]_t[k]
 //   ndig <= w < 2 ndig: [pt_d]_t[k] [a_{d,w-ndig}]_t[k]
 //   w = 2 ndig:         [P pt_d]_t[k] on q slots (t < lvl), else 0
-// pt null: 1 (a rotation).  Exact integers below 2^51 as doubles.
+// pt null: 1 (a rotation).  FP64 slots: the residues as doubles; integer
+// slots: Montgomery forms x 2^64 mod q, as 30-bit halves (gw_split) when every
+// integer modulus is below 2^60.
 // grid: (n / 256, nm, diagonals of this launch)
 // ---------------------------------------------------------------------------
 // words of one (diagonal, position) and the start of slot t's block (in
