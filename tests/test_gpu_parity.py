@@ -49,6 +49,10 @@ PARAMS = {
     # 61-bit q0 / P: integer moduli of 2^60 and above (the gemv's integer form
     # without its 30-bit-half products)
     "i14": ("params", dict(logn=14, nlimbs=6, nspecial=3, dnum=2, slots=64, q0_bits=61, qi_bits=48, p_bits=61)),
+    # five special primes (K > 4: no split key switch / fused ModDown) on an
+    # all-FP64 set: the gemv batch path's own ModUp (INTT, gemv_fbc_kernel,
+    # NTT) and the generic ModDown
+    "k5": ("params", dict(logn=13, nlimbs=4, nspecial=5, dnum=1, slots=64, q0_bits=51, qi_bits=48, p_bits=51)),
     # all-FP64 sets at n=2^13 and 2^15: the FP64 column kernels
     # ks_colsf<6, 8> / dn_colsf<6, .> / ntt2_colsf<6, .> (T = 64) and the
     # n=2^15 split-key-switch forms on every-modulus-below-2^51 primes

@@ -112,6 +112,7 @@ def run_batch(oracle, product, ko, kp, fn, host_in, out_words, *args):
                                                 ("bench51", 16, 4, 5), ("bench_d2", 16, 3, 8), ("bench_d2", 16, 17, 8),
                                                 ("bench_d2", 16, 4, 5), ("c5f", 16, 3, 12), ("c5f", 64, 2, 12),
                                                 ("c5", 16, 2, 12), ("c14", 16, 9, 6), ("c15", 16, 5, 6), ("i14", 16, 3, 6),
+                                                ("k5", 16, 3, 4),
                                                 ("c1", 16, 3, 4), ("hyb", 16, 3, 5)])
 def test_gemv_rot_batch(oracle, product, name, slots, cnt, lvl):
     """he_gemv_batch and he_rot_batch over `cnt` real encryptions at level
