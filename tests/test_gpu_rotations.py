@@ -176,3 +176,21 @@ def test_gemv_rot_batch_chunks_and_empty(oracle, product, monkeypatch):
     assert bool((dout == 7).all())
     for e, k in ((oracle, ko), (product, kp)):
         e.free_evks(k[2])
+
+
+def test_gemv_generic_path():
+    """GPQHE_GEMV_WIN=0 (read once per process, so in a child process): the
+    round-4 generic kernels (one ciphertext at a time, the baseline of
+    profiles/r5_gemv_baseline_generic*.json) stay bit-exact against the
+    oracle at the bench's shape."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPQHE_GEMV_WIN="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "gemv_switch_worker.py")], env=env, cwd=root,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert res == {"gemv_batch": 0, "rot_batch": 0}, res
