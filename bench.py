@@ -50,7 +50,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # one key for all ranks: the context / key replicas of every rank share these
 # seeds (the headline and 60-bit legs, and config 5)
-KEY_SEED, C5_KEY_SEED, GEMV_KEY_SEED = 1000, 2000, 3000
+KEY_SEED, C5_KEY_SEED, GEMV_KEY_SEED, C5_GEMV_KEY_SEED = 1000, 2000, 3000, 4000
 # kernels of the fused he_mul_rescale_batch pipeline (n = 2^16: one launch each per chunk)
 PIPELINE = ("d2_rows_kernel", "ks_cols4_kernel", "ksq_kernel<drop>", "dn_cols_kernel", "ksq_kernel<keep>")
 
@@ -78,6 +78,8 @@ def parse(argv=None):
     ap.add_argument("--c5-batch", type=int, default=64)
     ap.add_argument("--no-gemv", action="store_true", help="skip the he_gemv_batch / he_rot_batch leg")
     ap.add_argument("--gemv-batch", type=int, default=256)
+    ap.add_argument("--c5-gemv-batch", type=int, default=64,
+                    help="config 5 as a hempc batch: he_gemv_batch ciphertexts per GPU at N=2^17, L=12 (0: skip)")
     ap.add_argument("--gemv-slots", type=int, default=16, help="slots (HECTR's own: 16) = gemv diagonals")
     ap.add_argument("--ntt-polys", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample duration per thread count")
@@ -813,6 +815,55 @@ def gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
     return leg
 
 
+def c5_gemv_leg(args, stream, rank, world, red_dev, barrier, backend):
+    """Config 5 read as written (BASELINE configs[4]: "hempc ciphertext batch
+    sharded across 8 x MI355X, N=2^17, L=12"): he_gemv_batch -- hempc's
+    encrypted matrix-vector step, src/hempc.c:257,259 -- at N=2^17, L=12
+    (dnum 3, K 4, the headline's prime sizes), HECTR's 16 slots, each rank its
+    shard of one global batch under one key, no collective on the data path."""
+    from hectr_amd import dist as hdist
+    B, s = args.c5_gemv_batch, args.gemv_slots
+    steps = max(2, args.steps // 4)
+    gb = GemvBatch(stream, 17, 12, 3, args.q0_bits, args.p_bits, 4, s, B, rank * B, C5_GEMV_KEY_SEED)
+    gb.step()  # folds the rotation keys with the diagonals (cached)
+    gb.eng.sync()
+    t_all = hdist.all_values(timed(gb.step, steps, 1, gb.eng.sync, barrier), device=red_dev)
+    t = max(t_all)
+    gb.eng.prof_enable(True)
+    for _ in range(steps):
+        gb.step()
+    gb.eng.sync()
+    st = gb.eng.prof_collect()
+    gb.eng.prof_enable(False)
+    leg = None
+    if rank == 0:
+        v = world * B * steps / t
+        leg = {"workload": f"he_gemv_batch ({s} x {s} complex matrix, {s} non-zero diagonals), N=2^17, L=12, "
+                           f"K=4, dnum=3, primes {args.q0_bits}/50/{args.p_bits} bits, batch={B} ciphertexts per GPU",
+               "n_gpus": world, "value": v, "per_gpu_value": v / world, "unit": "gemv/s", "steps": steps,
+               "ms_per_step": 1e3 * t / steps, "us_per_gemv_per_gpu": 1e6 * world / v,
+               "rotations_in_gemv_per_s": v * (s - 1), "rank_times_s": t_all, "rank_time_min_s": min(t_all),
+               "rank_time_max_s": t,
+               "op_roofline_frac": gb.alg_bytes() * v / world / 1e9 / HBM_PEAK_GBS,
+               "kernels": {k: {"launches": w[0], "avg_us": w[1] / w[0], "us_per_gemv": w[1] / (steps * B)}
+                           for k, w in sorted(st.items(), key=lambda kv: -kv[1][1])}}
+    shard = gb.y.cpu() if args.check_shards else None
+    gb.close()
+    barrier()
+    if args.check_shards:
+        def ref(count):
+            r = GemvBatch(stream, 17, 12, 3, args.q0_bits, args.p_bits, 4, s, count, 0, C5_GEMV_KEY_SEED)
+            r.step()
+            r.eng.sync()
+            out = r.y.cpu()
+            r.close()
+            return out
+        chk = shard_check(shard, rank, world, backend, B, ref, key="cts")
+        if rank == 0:
+            leg["shard_check"] = chk
+    return leg
+
+
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
@@ -1011,6 +1062,10 @@ def main():
         g = gemv_leg(args, stream, rank, world, red_dev, barrier, backend)
         if rank == 0:
             result["gemv"] = g
+        if not args.no_c5 and args.c5_gemv_batch:
+            g5 = c5_gemv_leg(args, stream, rank, world, red_dev, barrier, backend)
+            if rank == 0:
+                result["config5"]["hempc_gemv"] = g5
 
     if rank == 0 and world == 1 and not args.no_cstr:
         result["cstr"] = cstr_loop(args.cstr_steps)

@@ -37,15 +37,16 @@ def test_bench_two_ranks_shards_bit_exact(streams):
 
 def test_bench_two_ranks_c5_and_gemv_shards_bit_exact():
     """The config-5 leg (N=2^17, L=12, dnum=3: 3 pairs per rank, split 1 + 2
-    over the two sub-chunk streams) and the gemv leg (he_gemv_batch at the
-    headline shape with HECTR's 16 slots, 3 ciphertexts per rank) at two
+    over the two sub-chunk streams), the gemv leg (he_gemv_batch at the
+    headline shape with HECTR's 16 slots, 3 ciphertexts per rank) and config
+    5 as a hempc batch (he_gemv_batch at N=2^17, L=12, 2 per rank) at two
     ranks: each leg's gathered output shards equal one context's run of its
     whole global batch, and the line reports every rank's time."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env["HECTR_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
            "1", "--no-cpu", "--no-cstr", "--no-ntt", "--alt-bits", "0", "--c5-batch", "3", "--gemv-batch", "3",
-           "--check-shards"]
+           "--c5-gemv-batch", "2", "--check-shards"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
@@ -55,6 +56,9 @@ def test_bench_two_ranks_c5_and_gemv_shards_bit_exact():
     assert c5["shard_check"] == {"pairs": 6, "ranks": 2, "bit_exact": True, "differing_pairs": []}, c5["shard_check"]
     assert g["shard_check"] == {"cts": 6, "ranks": 2, "bit_exact": True, "differing_cts": []}, g["shard_check"]
     assert len(c5["rank_times_s"]) == 2 and len(g["rank_times_s"]) == 2
+    h = c5["hempc_gemv"]  # config 5 as a hempc batch: he_gemv_batch at N=2^17, L=12
+    assert h["shard_check"] == {"cts": 4, "ranks": 2, "bit_exact": True, "differing_cts": []}, h["shard_check"]
+    assert len(h["rank_times_s"]) == 2
 
 
 def test_bench_two_ranks_default_legs():
@@ -65,13 +69,13 @@ def test_bench_two_ranks_default_legs():
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env["HECTR_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "3", "--steps", "2", "--warmup",
-           "1", "--c5-batch", "2", "--gemv-batch", "3"]
+           "1", "--c5-batch", "2", "--gemv-batch", "3", "--c5-gemv-batch", "2"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1
     d = lines[0]
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["value_60bit"] > 0
-    assert d["config5"]["value"] > 0 and d["config5"]["value_60bit"] > 0
+    assert d["config5"]["value"] > 0 and d["config5"]["value_60bit"] > 0 and d["config5"]["hempc_gemv"]["value"] > 0
     g = d["gemv"]
     assert g["value"] > 0 and g["alt_primes"]["value"] > 0 and len(g["rank_times_s"]) == 2
