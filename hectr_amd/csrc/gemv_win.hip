@@ -44,6 +44,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 __device__ __forceinline__ unsigned gw_brev(unsigned x, unsigned bits)
@@ -60,27 +61,21 @@ __device__ __forceinline__ unsigned gw_auto_index(unsigned k, uint64_t g, unsign
 }
 
 // ---------------------------------------------------------------------------
-// Folded keys, output order, interleaved: slot t's block at gw_kbase(t),
-// then [(e n + k) KW_t + w] for output position k (KW_t = 2 ndig + 2 on q
-// slots, the last word padding; 2 ndig on P slots, which have no P pt word):
+// Folded keys, output order, interleaved: slot t's block at gw_kbase(t), then
+// [(e n + k) 2 ndig + w] for output position k:
 //   w < ndig:           [pt_d]_t[k] [b_{d,w}]_t[k]
 //   ndig <= w < 2 ndig: [pt_d]_t[k] [a_{d,w-ndig}]_t[k]
-//   w = 2 ndig:         [P pt_d]_t[k] on q slots (t < lvl), else 0
+// and after all slots' blocks (gw_kbase(nm)) the q slots' P pt_d words,
+// [(t E + e) n + k] for t < lvl (gemv_c0_kernel; the identity's c1 term).
 // pt null: 1 (a rotation).  FP64 slots: the residues as doubles; integer
 // slots: Montgomery forms x 2^64 mod q, as 30-bit halves (gw_split) when every
 // integer modulus is below 2^60.
 // grid: (n / 256, nm, diagonals of this launch)
 // ---------------------------------------------------------------------------
-// words of one (diagonal, position) and the start of slot t's block (in
-// words, E diagonals)
-__host__ __device__ __forceinline__ unsigned gw_kw(unsigned t, unsigned lvl, unsigned ndig)
+// the start of slot t's key block (in words, E diagonals)
+__host__ __device__ __forceinline__ size_t gw_kbase(unsigned t, unsigned ndig, unsigned E, unsigned logn)
 {
-  return 2 * ndig + (t < lvl ? 2 : 0);
-}
-__host__ __device__ __forceinline__ size_t gw_kbase(unsigned t, unsigned lvl, unsigned ndig, unsigned E, unsigned logn)
-{
-  const unsigned tq = t < lvl ? t : lvl, tp = t - tq;
-  return ((size_t)tq * (2 * ndig + 2) + (size_t)tp * 2 * ndig) * E << logn;
+  return ((size_t)t * 2 * ndig * E) << logn;
 }
 
 struct FoldArgs {
@@ -100,14 +95,14 @@ __host__ __device__ __forceinline__ uint64_t gw_split(uint64_t x)
 
 __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, unsigned Etot, unsigned ndig,
                                                         unsigned logn, unsigned lvl, unsigned L, unsigned nmod,
-                                                        const ModConst *mcs)
+                                                        unsigned nm, const ModConst *mcs)
 {
   const unsigned k = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y, e = blockIdx.z;
   const unsigned m = basis_mod(t, lvl, L);
   const ModConst mc = mcs[m];
   const uint64_t *pt = fa.pt[e], *ev = fa.evk[e];
   const uint64_t w = pt ? pt[((size_t)t << logn) + k] : 1;
-  const unsigned kw = gw_kw(t, lvl, ndig);
+  const unsigned kw = 2 * ndig;
   const bool isint = (fa.intmask >> t) & 1;
   // FP64 slots: the residue as a double; integer slots: its Montgomery form
   // x 2^64 mod q (bits), so the kernel's REDC of y x returns y x mod q
@@ -119,15 +114,13 @@ __global__ void __launch_bounds__(256) gemv_fold_kernel(double *K, FoldArgs fa, 
       *(uint64_t *)o = (uint64_t)__double_as_longlong((double)v);
     }
   };
-  double *o = K + gw_kbase(t, lvl, ndig, Etot, logn) + ((((size_t)fa.e0 + e) << logn) + k) * kw;
+  double *o = K + gw_kbase(t, ndig, Etot, logn) + ((((size_t)fa.e0 + e) << logn) + k) * kw;
   for (unsigned j = 0; j < ndig; j++) {
     put(o + j, ev ? mul_mod(w, ev[(((size_t)(2 * j) * nmod + m) << logn) + k], mc) : 0);
     put(o + ndig + j, ev ? mul_mod(w, ev[(((size_t)(2 * j + 1) * nmod + m) << logn) + k], mc) : 0);
   }
-  if (t < lvl) {
-    put(o + 2 * ndig, mul_mod(w, mc.pmod, mc));
-    put(o + 2 * ndig + 1, 0);
-  }
+  if (t < lvl)
+    put(K + gw_kbase(nm, ndig, Etot, logn) + ((((size_t)t * Etot + fa.e0 + e) << logn) + k), mul_mod(w, mc.pmod, mc));
 }
 
 // ---------------------------------------------------------------------------
@@ -185,7 +178,8 @@ struct GemvWin {
   size_t x_stride, x_pstride;
   const uint64_t *Dc;  // compact ModUp digits [count][S][n]
   size_t d_stride;
-  const double *K;  // folded keys [nm][Etot][n][2 ndig + 2]
+  const double *K;   // folded keys (gw_kbase: [nm][Etot][n][2 ndig])
+  const double *Kp;  // the q slots' P pt_d words [lvl][Etot][n]
   uint64_t *acc;    // [count][2][nm][n]
   size_t acc_stride;
   int16_t yi[GPQHE_MAXMOD / 2][3];  // slot t, digit j: its Dc slot, -1: the own digit (c1 limb t)
@@ -239,11 +233,17 @@ __global__ void __launch_bounds__(256) gemv_tab_kernel(uint32_t *tab, GemvTab ta
 }
 
 // C ciphertexts per workgroup share every key word a lane loads (the keys'
-// L2 traffic is the kernel's largest: C = 3 where the ring fits, 144 KB)
-template <int NDIG>
+// L2 traffic is the kernel's largest): as many as the ring (C x 32 blocks x
+// ndig words x 512 B) and the registers allow -- the c0 term runs in its own
+// pass (gemv_c0_kernel), so the ring holds the digits only: two digits 4
+// ciphertexts (128 KB) against 3 with c0 in the ring (inner products 31.5 ->
+// 24.5 us per ciphertext at N=2^16, L=8, 16 slots, same box), three digits 3
+// (144 KB) against 2. With C0IN (the c0 word in the ring): 3 for two digits,
+// 2 for three (and for one: 3 spills there)
+template <int NDIG, bool C0IN = false>
 constexpr int gw_cts()
 {
-  return NDIG >= 3 ? 2 : 3;
+  return C0IN ? (NDIG != 2 ? 2 : 3) : (NDIG >= 3 ? 3 : 4);
 }
 
 // One ring word: a centred double (FP64 slots) or a canonical residue
@@ -298,18 +298,24 @@ struct GwAcc3 {
 // INT: the slots of this launch are on 64-bit integer moduli (q >= 2^51: the
 // 60-bit q_0 / P of HECTR-like prime sets).  Their key words are Montgomery
 // forms (gemv_fold_kernel), a diagonal's products are summed in 128 bits
-// (at most 2 ndig + 1 < 2^4 products of residues below q < 2^60: below
-// q 2^64) and reduced by one REDC, the accumulators kept in [0, 2q).
+// (at most ndig + 1 <= 4 products of residues below q < 2^61: below q 2^64)
+// and reduced by one REDC, the accumulators kept in [0, 2q).
 // LZ (FP64 slots with q < 2^50, at most two digits; chosen per workgroup
 // around the advance loop): the accumulators are reduced every third diagonal
 // instead of every one.  With centred ring values
 // |y| <= q/2 < 2^49 a product is below q (1/2 + 1.5 |y| 2^-52) < 0.69 q, so
-// three diagonals of three products on top of |acc| <= q/2 stay below 6.9 q
-// < 2^52.8 (and one more canonical word added at the output below 2^53).
-template <int NDIG, int W, bool INT, bool SPLIT = false>
+// three diagonals of two products (three with C0IN's c0 term) on top of
+// |acc| <= q/2 stay below 4.7 q < 2^52.3 (6.9 q < 2^52.8), and one more
+// canonical word added at the output below 2^53.
+// C0IN: the q slots' c0 term in this kernel (c0 a ring word, its P pt_d word
+// from a.Kp per diagonal) instead of gemv_c0_kernel's pass -- the form for
+// three digits (a fourth ring word costs one ciphertext per workgroup, 3 -> 2,
+// against a separate pass that measured slower there) and for launches of a
+// few diagonals (a rotation: the separate pass's fixed cost).
+template <int NDIG, int W, bool INT, bool SPLIT = false, bool C0IN = false>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
-  constexpr int C = gw_cts<NDIG>(), RING = 32, NWD = NDIG + 1, KW = 2 * NDIG + 2;
+  constexpr int C = gw_cts<NDIG, C0IN>(), RING = 32, NWD = NDIG + (C0IN ? 1 : 0), KW = 2 * NDIG;
   __shared__ GwWord ring[C][RING][NWD][64];
   const unsigned logn = a.logn, bb = logn - 6, P = 1u << (bb - 1);
   const unsigned nmem = (a.count + C - 1) / C;
@@ -332,7 +338,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 #pragma unroll
   for (int e = 0; e < W; e++)
     gj[e] = e < E ? (a.hm[e] * jh) & 63 : 0;
-  // the ring words: digit j (its ModUp limb, or c1 for the own digit), c0
+  // the ring words: digit j (its ModUp limb, or c1 for the own digit)
   const uint64_t *sp[C][NWD];
 #pragma unroll
   for (int c = 0; c < C; c++) {
@@ -343,10 +349,13 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       const int yi = a.yi[t][j];
       sp[c][j] = yi < 0 ? xb + a.x_pstride + ((size_t)t << logn) : a.Dc + (size_t)pc * a.d_stride + ((size_t)yi << logn);
     }
-    sp[c][NDIG] = xb + ((size_t)(qs ? t : 0) << logn);
+    if constexpr (C0IN)
+      sp[c][NWD - 1] = xb + ((size_t)(qs ? t : 0) << logn);
   }
-  const unsigned kwt = qs ? KW : KW - 2;  // P slots: no P pt word, no padding
-  const double *Kt = a.K + gw_kbase(t, a.lvl, NDIG, a.Etot, logn) + ((size_t)a.e0 << logn) * kwt;
+  const double *Kt = a.K + gw_kbase(t, NDIG, a.Etot, logn) + ((size_t)a.e0 << logn) * KW;
+  // the q slots' [P pt_d] words (the identity's c1 term; with C0IN every
+  // diagonal's c0 term -- else gemv_c0_kernel's)
+  const double *Kpid = a.Kp + (((size_t)(qs ? t : 0) * a.Etot + a.e0) << logn);
   const size_t apoly = (size_t)a.nm << logn;
   const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
   uint64_t pv[C][NWD];
@@ -356,7 +365,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     for (int c = 0; c < C; c++)
 #pragma unroll
       for (int w = 0; w < NWD; w++)
-        pv[c][w] = (w < NDIG || qs) ? sp[c][w][off] : 0;
+        pv[c][w] = sp[c][w][off];  // (C0IN P slots: slot 0's c0, unused)
   };
   auto store_src = [&](unsigned s) {
     const unsigned slot = s & (RING - 1);
@@ -401,39 +410,47 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       // one diagonal at a time (the body is too long to unroll over 16: a
       // register array indexed by the diagonal would go to scratch); the
       // next diagonal's key words in flight meanwhile
-      uint64_t kc[KW], kn[KW];
-      auto load_keys = [&](int e, uint64_t (&kk)[KW]) {
-        const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * kwt);
+      uint64_t kc[KW + 1], kn[KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
+      auto load_keys = [&](int e, uint64_t (&kk)[KW + 1]) {
+        const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
 #pragma unroll
         for (int w = 0; w < KW / 2; w++) {
-          const ulonglong2 v = (w < NDIG || qs) ? kp[w] : make_ulonglong2(0, 0);
+          const ulonglong2 v = kp[w];
           kk[2 * w] = v.x;
           kk[2 * w + 1] = v.y;
         }
+        kk[KW] = C0IN && qs ? ((const uint64_t *)Kpid)[((size_t)e << logn) + koff] : 0;
       };
       load_keys(0, kn);
       for (int e = 0; e < E; e++) {
 #pragma unroll
-        for (int w = 0; w < KW; w++)
+        for (int w = 0; w <= KW; w++)
           kc[w] = kn[w];
         if (e + 1 < E)
           load_keys(e + 1, kn);
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
-        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
+        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots (c0 here only with C0IN)
           if (qs) {
+            const uint64_t kpi = ((const uint64_t *)Kpid)[koff];
 #pragma unroll
             for (int c = 0; c < C; c++) {
-              const uint64_t y0 = ring[c][slot][NDIG][sl].u, y1 = ring[c][slot][jo][sl].u;
+              const uint64_t y1 = ring[c][slot][jo][sl].u;
               if constexpr (SPLIT) {
-                GwAcc3 b0, b1;
-                b0.mac(y0, kc[2 * NDIG]);
-                b1.mac(y1, kc[2 * NDIG]);
-                u0[c] = b0.redc(qi, qni);
+                GwAcc3 b1;
+                b1.mac(y1, kpi);
                 u1[c] = b1.redc(qi, qni);
+                if constexpr (C0IN) {
+                  GwAcc3 b0;
+                  b0.mac(ring[c][slot][NDIG][sl].u, kpi);
+                  u0[c] = b0.redc(qi, qni);
+                }
               } else {
-                u0[c] = gw_redc(mulhi64(y0, kc[2 * NDIG]), y0 * kc[2 * NDIG], qi, qni);
-                u1[c] = gw_redc(mulhi64(y1, kc[2 * NDIG]), y1 * kc[2 * NDIG], qi, qni);
+                u1[c] = gw_redc(mulhi64(y1, kpi), y1 * kpi, qi, qni);
+                if constexpr (C0IN) {
+                  const uint64_t y0 = ring[c][slot][NDIG][sl].u;
+                  u0[c] = gw_redc(mulhi64(y0, kpi), y0 * kpi, qi, qni);
+                }
               }
             }
           }
@@ -449,8 +466,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
               b0.mac(yv, kc[j]);
               b1.mac(yv, kc[NDIG + j]);
             }
-            if (qs)
-              b0.mac(ring[c][slot][NDIG][sl].u, kc[2 * NDIG]);
+            if (C0IN && qs)
+              b0.mac(ring[c][slot][NWD - 1][sl].u, kc[KW]);
             u0[c] = lazy_lt2q(u0[c] + b0.redc(qi, qni), q2);
             u1[c] = lazy_lt2q(u1[c] + b1.redc(qi, qni), q2);
           }
@@ -465,8 +482,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
             gw_mac128(h0, l0, yv, kc[j]);
             gw_mac128(h1, l1, yv, kc[NDIG + j]);
           }
-          if (qs)
-            gw_mac128(h0, l0, ring[c][slot][NDIG][sl].u, kc[2 * NDIG]);
+          if (C0IN && qs)
+            gw_mac128(h0, l0, ring[c][slot][NWD - 1][sl].u, kc[KW]);
           u0[c] = lazy_lt2q(u0[c] + gw_redc(h0, l0, qi, qni), q2);
           u1[c] = lazy_lt2q(u1[c] + gw_redc(h1, l1, qi, qni), q2);
         }
@@ -475,18 +492,22 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     // key words two diagonals ahead (a ring of three sets): the L2 latency of
     // a diagonal's keys overlaps the two before it
     constexpr int KD = 3;
-    uint64_t kw[KD][KW];
+    uint64_t kw[KD][KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
     auto load_keys = [&](int e) {
 #ifdef GW_EXP_NOKEY  // (timing experiment: every diagonal takes diagonal 0's keys)
-      const ulonglong2 *kp = (const ulonglong2 *)(Kt + koff * kwt);
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + koff * KW);
 #else
-      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * kwt);
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
 #endif
 #pragma unroll
       for (int w = 0; w < KW / 2; w++) {
-        const ulonglong2 v = (w < NDIG || qs) ? kp[w] : make_ulonglong2(0, 0);
+        const ulonglong2 v = kp[w];
         kw[e % KD][2 * w] = v.x;
         kw[e % KD][2 * w + 1] = v.y;
+      }
+      if constexpr (C0IN) {  // (P slots: zero -- the product below adds nothing)
+        const uint64_t v = ((const uint64_t *)Kpid)[((size_t)e << logn) + koff];
+        kw[e % KD][KW] = qs ? v : 0;
       }
     };
 #pragma unroll
@@ -502,12 +523,14 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         auto k = [&](int w) { return __longlong_as_double((long long)ku[w]); };
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + gj[e]) & 63, 6);  // the lane of this output's source
-        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots
+        if (ident && e == 0) {  // the identity: [P pt_0] (c0 with C0IN, c1) on q slots
           if (qs) {
+            const double kpi = Kpid[koff];
 #pragma unroll
             for (int c = 0; c < C; c++) {
-              a0[c] = f64_mulmod_h(ring[c][slot][NDIG][sl].d, k(2 * NDIG), q, qinv);
-              a1[c] = f64_mulmod_h(ring[c][slot][jo][sl].d, k(2 * NDIG), q, qinv);
+              a1[c] = f64_mulmod_h(ring[c][slot][jo][sl].d, kpi, q, qinv);
+              if constexpr (C0IN)
+                a0[c] = f64_mulmod_h(ring[c][slot][NWD - 1][sl].d, kpi, q, qinv);
             }
           }
         } else {
@@ -528,8 +551,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
               s0 += f64_mulmod_h(yv, k(j), q, qinv);
               s1 += f64_mulmod_h(yv, k(NDIG + j), q, qinv);
             }
-            if (qs)
-              s0 += f64_mulmod_h(ring[c][slot][NDIG][sl].d, k(2 * NDIG), q, qinv);
+            if constexpr (C0IN)
+              s0 += f64_mulmod_h(ring[c][slot][NWD - 1][sl].d, k(KW), q, qinv);
             if (!LZ || NDIG > 2 || e % 3 == 2) {
               a0[c] = f64_red(s0, q, qinv);  // (|s0| < 3.2 q before; LZ: < 6.9 q)
               a1[c] = f64_red(s1, q, qinv);
@@ -571,6 +594,134 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     advances(std::true_type{});
   else
     advances(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------
+// The c0 term of the q slots: acc0[t][k] += sum_d [P pt_d]_t[k] c0[pi_d k],
+// run after the digit inner products of the same diagonals (gemv_win_kernel)
+// with the same orbit walk and LDS ring, one ring word per ciphertext, so a
+// workgroup carries 8 ciphertexts per key word.  The P pt_d words are the
+// fold's separate q-slot array (a.Kp).
+// FP64: |product| <= 0.875 q (centred ring values, q < 2^51); reduced every
+// second diagonal, so |acc| < 2.25 q, and < 3.25 q with the word it adds to.
+// ---------------------------------------------------------------------------
+template <int W, bool INT, bool SPLIT>
+__global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
+{
+  constexpr int C = 8, RING = 32, KD = 3;
+  __shared__ GwWord ring[C][RING][64];
+  const unsigned logn = a.logn, bb = logn - 6, P = 1u << (bb - 1);
+  const unsigned nmem = (a.count + C - 1) / C;
+  unsigned grp, mi;
+  if (!xcd_group(nmem, a.ns * 2 * a.nseg, grp, mi))
+    return;
+  const unsigned t = a.slot[grp / (2 * a.nseg)], orb = (grp / a.nseg) & 1, seg = grp % a.nseg;
+  const unsigned SEG = P / a.nseg, o0 = seg * SEG;
+  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
+  const unsigned p0 = mi * C;
+  const unsigned nc = min((unsigned)C, a.count - p0);
+  const double q = a.md.q[t], qinv = a.md.qinv[t];
+  const uint64_t qi = a.md.qi[t], qni = a.md.qni[t], q2 = 2 * qi;
+  const int E = (int)a.E, dmin = a.d[0], dmax = a.d[E - 1];
+  const unsigned jh = gw_brev(L, 6);
+  const uint64_t *sp[C];
+#pragma unroll
+  for (int c = 0; c < C; c++)
+    sp[c] = a.x + (size_t)(p0 + ((unsigned)c < nc ? c : 0)) * a.x_stride + ((size_t)t << logn);
+  const uint64_t *Kpt = (const uint64_t *)a.Kp + (((size_t)t * a.Etot + a.e0) << logn);
+  const uint32_t *tabo = a.tab + (size_t)orb * P * 32;
+  uint64_t pv[C];
+  auto load_src = [&](unsigned s) {
+    const size_t off = ((size_t)tabo[(s & (P - 1)) * 32 + 16] << 6) + L;
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      pv[c] = sp[c][off];
+  };
+  auto store_src = [&](unsigned s) {
+    const unsigned slot = s & (RING - 1);
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      if constexpr (INT)
+        ring[c][slot][L].u = SPLIT ? gw_split(pv[c]) : pv[c];
+      else
+        ring[c][slot][L].d = gw_center(f64_from_u52(pv[c]), q);
+    }
+  };
+  const unsigned nadv = SEG / 16;
+  for (unsigned adv = 0; adv < nadv; adv++) {
+    const unsigned ob = o0 + adv * 16;
+    if (adv == 0) {
+      for (unsigned s = ob + dmin + wv; s < ob + 16 + dmax; s += 16) {
+        load_src(s);
+        store_src(s);
+      }
+    } else {
+      store_src(ob + dmax + wv);
+    }
+    __syncthreads();
+    if (adv + 1 < nadv)
+      load_src(ob + 16 + dmax + wv);
+    const unsigned o = ob + wv;
+    const uint32_t *tr = tabo + (o & (P - 1)) * 32;
+    const size_t koff = ((size_t)tr[16] << 6) + L;
+    // the accumulator words this advance updates, requested before its products
+    uint64_t av[C];
+#pragma unroll
+    for (int c = 0; c < C; c++)
+      av[c] = (unsigned)c < nc ? a.acc[(size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff] : 0;
+    double f[C];
+    uint64_t u[C];
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      f[c] = 0.0;
+      u[c] = 0;
+    }
+    uint64_t kd[KD];
+#pragma unroll
+    for (int e = 0; e < KD - 1; e++)
+      if (e < E)
+        kd[e] = Kpt[((size_t)e << logn) + koff];
+#pragma unroll
+    for (int e = 0; e < W; e++) {
+      if (e < E) {
+        if (e + KD - 1 < W && e + KD - 1 < E)
+          kd[(e + KD - 1) % KD] = Kpt[((size_t)(e + KD - 1) << logn) + koff];
+        const uint64_t kw = kd[e % KD];
+        const unsigned slot = (o + a.d[e]) & (RING - 1);
+        const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+          if constexpr (INT) {
+            const uint64_t y = ring[c][slot][sl].u;
+            uint64_t r;
+            if constexpr (SPLIT) {
+              GwAcc3 b;
+              b.mac(y, kw);
+              r = b.redc(qi, qni);
+            } else {
+              r = gw_redc(mulhi64(y, kw), y * kw, qi, qni);
+            }
+            u[c] = lazy_lt2q(u[c] + r, q2);
+          } else {
+            f[c] += f64_mulmod_h(ring[c][slot][sl].d, __longlong_as_double((long long)kw), q, qinv);
+            if (e & 1)
+              f[c] = f64_red(f[c], q, qinv);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      if ((unsigned)c >= nc)
+        continue;
+      uint64_t *op = a.acc + (size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff;
+      if constexpr (INT)
+        op[0] = add_mod(u[c] >= qi ? u[c] - qi : u[c], av[c], qi);
+      else
+        op[0] = f64_canon(f[c] + f64_from_u52(av[c]), q, qinv);
+    }
+    __syncthreads();  // the ring slots the next advance overwrites were read here
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -644,7 +795,7 @@ static void gw_galois(unsigned d, uint64_t &g, uint64_t &gi)
 size_t k_gemv_fold_words(unsigned E, unsigned lvl)
 {
   const unsigned ndig = (lvl + G.alpha - 1) / G.alpha, nm = lvl + G.K;
-  return gw_kbase(nm, lvl, ndig, E, G.logn);
+  return gw_kbase(nm, ndig, E, G.logn) + ((size_t)lvl * E << G.logn);
 }
 
 double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
@@ -663,7 +814,7 @@ double *k_gemv_fold(const GemvDiagIn *dg, unsigned E, unsigned lvl)
     }
     ProfScope ps(KC_GEMV_FOLD, 8.0 * G.n * cnt * nm * ((double)(2 * ndig + 1) + (2 * ndig + 2)));
     hipLaunchKernelGGL(gemv_fold_kernel, dim3(G.n / 256, nm, cnt), dim3(256), 0, G.stream, K, fa, E, ndig, G.logn, lvl,
-                       G.L, G.nmod, G.dev.mc);
+                       G.L, G.nmod, nm, G.dev.mc);
     HIP_CHECK(hipGetLastError());
   }
   return K;
@@ -734,7 +885,10 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   // 4. the inner products, diagonals in launches spanning at most 16
   // rotations (the LDS ring: 16 output blocks and the 15 more sources they
   // read); segments of >= 16 blocks, enough workgroups to fill the chip
-  const unsigned P = 1u << (logn - 7), cpw = ndig >= 3 ? 2 : 3;  // (cpw: gw_cts)
+  // the c0 term in the main kernel (C0IN) for three digits and for a few
+  // diagonals, else in gemv_c0_kernel's pass (see gemv_win_kernel)
+  const bool c0in = ndig >= 3 || E < 4;
+  const unsigned P = 1u << (logn - 7), cpw = c0in ? (ndig != 2 ? 2 : 3) : (ndig >= 3 ? 3 : 4);  // (cpw: gw_cts)
   unsigned nseg = 1;
   while (nseg < P / 16 && (size_t)nm * 2 * nseg * ((cnt + cpw - 1) / cpw) < 1024)
     nseg *= 2;
@@ -745,6 +899,7 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   a.Dc = Dc;
   a.d_stride = ds;
   a.K = K;
+  a.Kp = K + gw_kbase(nm, ndig, E, logn);
   a.acc = acc;
   a.acc_stride = as;
   for (unsigned t = 0; t < nm; t++)
@@ -761,10 +916,16 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
   // the basis slots by arithmetic class: one launch per class and diagonal run
   const uint64_t imask = gw_intmask(lvl);
   GemvWin acls[2] = {a, a};  // [0] FP64 slots, [1] integer slots
+  GemvWin qcls[2] = {a, a};  // their q slots (the c0 term)
   for (unsigned t = 0; t < nm; t++) {
     GemvWin &c = acls[(imask >> t) & 1];
     c.slot[c.ns++] = (uint8_t)t;
+    if (t < lvl) {
+      GemvWin &cq = qcls[(imask >> t) & 1];
+      cq.slot[cq.ns++] = (uint8_t)t;
+    }
   }
+  const bool split = gw_split_ok(lvl);
   uint32_t *tab = (uint32_t *)pool_alloc((size_t)2 * P * 32 * 4);
   bool first = true;
   for (unsigned e0 = 0; e0 < E;) {
@@ -787,32 +948,74 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     hipLaunchKernelGGL(gemv_tab_kernel, dim3((2 * P * 32 + 255) / 256), dim3(256), 0, G.stream, tab, ta);
     HIP_CHECK(hipGetLastError());
     a.tab = tab;
+    auto setup = [&](GemvWin &c) {
+      memcpy(c.d, a.d, sizeof a.d);
+      memcpy(c.hm, a.hm, sizeof a.hm);
+      c.tab = a.tab;
+      c.E = a.E;
+      c.e0 = a.e0;
+      c.accumulate = a.accumulate;
+    };
     {
-      // reads each ciphertext's ModUp digits and c0 once, the folded keys once
-      // per slot and orbit, writes (or updates) the accumulators
-      ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + lvl + (first ? 2.0 : 4.0) * nm) +
-                                           (double)a.E * nm * (2 * ndig + 1)));
+      // reads each ciphertext's ModUp digits once, the folded keys once per
+      // slot, orbit and ciphertext group, writes (or updates) the accumulators
+      ProfScope ps(KC_GEMV_WIN, 8.0 * n * ((double)cnt * (ndig * nm + (c0in ? lvl : 0) + (first ? 2.0 : 4.0) * nm) +
+                                           (double)a.E * (nm * 2 * ndig + (c0in ? lvl : 0))));
       for (int ic = 0; ic < 2; ic++) {
         GemvWin &c = acls[ic];
         if (!c.ns)
           continue;
-        memcpy(c.d, a.d, sizeof a.d);
-        memcpy(c.hm, a.hm, sizeof a.hm);
-        c.tab = a.tab;
-        c.E = a.E;
-        c.e0 = a.e0;
-        c.accumulate = a.accumulate;
+        setup(c);
         const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, c.ns * 2 * nseg));
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, G.stream, c); };
-        const bool split = gw_split_ok(lvl);
-        switch (ndig * 2 + ic) {
-        case 2: go(gemv_win_kernel<1, 16, false>); break;
-        case 3: split ? go(gemv_win_kernel<1, 16, true, true>) : go(gemv_win_kernel<1, 16, true>); break;
-        case 4: go(gemv_win_kernel<2, 16, false>); break;
-        case 5: split ? go(gemv_win_kernel<2, 16, true, true>) : go(gemv_win_kernel<2, 16, true>); break;
-        case 6: go(gemv_win_kernel<3, 16, false>); break;
-        default: split ? go(gemv_win_kernel<3, 16, true, true>) : go(gemv_win_kernel<3, 16, true>); break;
+        auto form = [&](auto c0) {
+          constexpr bool C0 = decltype(c0)::value;
+          switch (ndig * 2 + ic) {
+          case 2: go(gemv_win_kernel<1, 16, false, false, C0>); break;
+          case 3: split ? go(gemv_win_kernel<1, 16, true, true, C0>) : go(gemv_win_kernel<1, 16, true, false, C0>); break;
+          case 4: go(gemv_win_kernel<2, 16, false, false, C0>); break;
+          case 5: split ? go(gemv_win_kernel<2, 16, true, true, C0>) : go(gemv_win_kernel<2, 16, true, false, C0>); break;
+          default: break;
+          }
+        };
+        if (ndig >= 3) {  // (always C0IN)
+          if (!ic)
+            go(gemv_win_kernel<3, 16, false, false, true>);
+          else if (split)
+            go(gemv_win_kernel<3, 16, true, true, true>);
+          else
+            go(gemv_win_kernel<3, 16, true, false, true>);
+        } else if (c0in) {
+          form(std::true_type{});
+        } else {
+          form(std::false_type{});
         }
+        HIP_CHECK(hipGetLastError());
+      }
+    }
+    if (!c0in) {
+      // the q slots' c0 term: reads c0 once per ciphertext, the P pt_d words
+      // once per slot, orbit and group of 8, updates the accumulators' poly 0
+      ProfScope ps(KC_GEMV_C0, 8.0 * n * ((double)cnt * 3.0 * lvl + (double)a.E * lvl));
+      for (int ic = 0; ic < 2; ic++) {
+        GemvWin &c = qcls[ic];
+        if (!c.ns)
+          continue;
+        setup(c);
+        // segments: one workgroup per CU at least (the c0 pass streams; its
+        // ring fill at each segment start is not hidden by compute)
+        unsigned nseg0 = 1;
+        while (nseg0 < P / 16 && (size_t)c.ns * 2 * nseg0 * ((cnt + 7) / 8) < 256)
+          nseg0 *= 2;
+        c.nseg = nseg0;
+        const dim3 grid(xcd_blocks((cnt + 7) / 8, c.ns * 2 * nseg0));
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, G.stream, c); };
+        if (!ic)
+          go(gemv_c0_kernel<16, false, false>);
+        else if (split)
+          go(gemv_c0_kernel<16, true, true>);
+        else
+          go(gemv_c0_kernel<16, true, false>);
         HIP_CHECK(hipGetLastError());
       }
     }

@@ -450,7 +450,7 @@ enum KClass {
   KC_NTT_WHOLE_FWD, KC_NTT_WHOLE_INV, KC_MODUP, KC_KS_INNER, KC_TENSOR, KC_DOWN_CONV, KC_DOWN_COMBINE, KC_KS_COLS,
   KC_KS_ROWS, KC_DN_COLS, KC_DN_ROWS, KC_D2_ROWS, KC_NTT2_COLS_FWD, KC_NTT3_ROWS_FWD, KC_NTT3_ROWS_INV,
   KC_NTT2_COLS_INV, KC_KS_COLS4, KC_NTT_SMALL_FWD, KC_NTT_SMALL_INV, KC_GEMV_INNER, KC_KSQ_DROP, KC_KSQ_KEEP,
-  KC_MODUP_SMALL, KC_DOWN_SMALL, KC_GEMV_WIN, KC_GEMV_FBC, KC_GEMV_FOLD, KC_COUNT
+  KC_MODUP_SMALL, KC_DOWN_SMALL, KC_GEMV_WIN, KC_GEMV_FBC, KC_GEMV_FOLD, KC_GEMV_C0, KC_COUNT
 };
 struct ProfScope {
   int cls;

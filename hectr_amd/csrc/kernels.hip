@@ -48,7 +48,7 @@ static const char *kc_names[KC_COUNT] = {
   "d2_rows_kernel", "ntt2_cols_kernel<fwd>", "ntt3_rows_kernel<fwd>", "ntt3_rows_kernel<inv>",
   "ntt2_cols_kernel<inv>", "ks_cols4_kernel", "ntt_small_kernel<fwd>", "ntt_small_kernel<inv>",
   "gemv_inner_kernel", "ksq_kernel<drop>", "ksq_kernel<keep>", "modup_small_kernel", "moddown_small_kernel",
-  "gemv_win_kernel", "gemv_fbc_kernel", "gemv_fold_kernel"};
+  "gemv_win_kernel", "gemv_fbc_kernel", "gemv_fold_kernel", "gemv_c0_kernel"};
 
 struct ProfEntry {
   int cls;
