@@ -40,12 +40,6 @@
 #ifndef KSQ_C5_DROP_LTW
 #define KSQ_C5_DROP_LTW 2
 #endif
-// timing experiments on the kept slots' kernel only (wrong outputs; variant
-// builds, never the default): 1 = no row passes, 2 = no loads of T1, the
-// inputs and conv (register values instead)
-#ifndef KSQ_EXP_KEEP
-#define KSQ_EXP_KEEP 0
-#endif
 
 // ===========================================================================
 // Key switch split at the ModDown boundary, key tile shared by quarter streams.
@@ -153,7 +147,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
     const uint64_t *s = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      x[k] = (KEEP && KSQ_EXP_KEEP == 2) ? (uint64_t)(th + k + p) : s[(row << LOGN2) + l + T::TA * k];
+      x[k] = s[(row << LOGN2) + l + T::TA * k];
   };
   unsigned p = pb0 + qi;
   uint64_t xn[NX > 0 ? NX : 1][8];
@@ -220,8 +214,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int a = 0; a < 4; a++) {
           const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4 * h);
-          const ulonglong2 w0 = (KEEP && KSQ_EXP_KEEP == 2) ? make_ulonglong2(th + a, p + h) : v2[0];
-          const ulonglong2 w1 = (KEEP && KSQ_EXP_KEEP == 2) ? make_ulonglong2(th + h, p + a) : v2[1];
+          const ulonglong2 w0 = v2[0];
+          const ulonglong2 w1 = v2[1];
           inw[a][0] = w0.x;
           inw[a][1] = w0.y;
           inw[a][2] = w1.x;
@@ -256,8 +250,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
         if (pn < pb1)
           fetch(xn[u], j, pn);  // next pair's tile, in flight meanwhile
         wave_sync();            // the previous phase has finished with the LDS tile
-        if constexpr (!(KEEP && KSQ_EXP_KEEP == 1))
-          rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
+        rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
         if constexpr (F) {
 #pragma unroll
           for (int k = 0; k < 8; k++) {
@@ -347,11 +340,9 @@ __global__ void __launch_bounds__(256 * QN, 1)
           V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            r[k] = A::load_lazy((KEEP && KSQ_EXP_KEEP == 2) ? (uint64_t)(th + k + half)
-                                : EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
+            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
           wave_sync();
-          if constexpr (!(KEEP && KSQ_EXP_KEEP == 1))
-            rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
+          rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           // out = f D^-1 - NTTrows(conv D^-1): both factors already folded in
           uint64_t o[8];
           if constexpr (F) {
