@@ -312,6 +312,9 @@ struct GwAcc3 {
 // three digits (a fourth ring word costs one ciphertext per workgroup, 3 -> 2,
 // against a separate pass that measured slower there) and for launches of a
 // few diagonals (a rotation: the separate pass's fixed cost).
+#ifndef GW_SRC_AT
+#define GW_SRC_AT 8
+#endif
 template <int NDIG, int W, bool INT, bool SPLIT = false, bool C0IN = false>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
@@ -393,8 +396,14 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       store_src(ob + dmax + wv);  // prefetched during the previous advance
     }
     __syncthreads();
-    if (adv + 1 < nadv)
-      load_src(ob + 16 + dmax + wv);  // the next advance's new block, in flight meanwhile
+    // the next advance's new block, requested at diagonal e_src (in flight
+    // over the rest of the advance): loads return in order, so requested
+    // before the first diagonals' key words it would hold them up, and every
+    // wave of the workgroup would wait out its HBM latency together
+    const bool more = adv + 1 < nadv;
+    const int e_src = min(GW_SRC_AT, E - 1);
+    if (GW_SRC_AT < 0 && more)
+      load_src(ob + 16 + dmax + wv);
     const unsigned o = ob + wv;
     const uint32_t *tr = tabo + (o & (P - 1)) * 32;
     const size_t koff = ((size_t)tr[16] << 6) + L;
@@ -428,6 +437,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
           kc[w] = kn[w];
         if (e + 1 < E)
           load_keys(e + 1, kn);
+        if (GW_SRC_AT >= 0 && e == e_src && more)
+          load_src(ob + 16 + dmax + wv);
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
         if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots (c0 here only with C0IN)
@@ -494,11 +505,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     constexpr int KD = 3;
     uint64_t kw[KD][KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
     auto load_keys = [&](int e) {
-#ifdef GW_EXP_NOKEY  // (timing experiment: every diagonal takes diagonal 0's keys)
-      const ulonglong2 *kp = (const ulonglong2 *)(Kt + koff * KW);
-#else
       const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
-#endif
 #pragma unroll
       for (int w = 0; w < KW / 2; w++) {
         const ulonglong2 v = kp[w];
@@ -519,6 +526,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       if (!INT && e < E) {
         if (e + KD - 1 < W && e + KD - 1 < E)
           load_keys(e + KD - 1);
+        if (GW_SRC_AT >= 0 && e == e_src && more)
+          load_src(ob + 16 + dmax + wv);
         const uint64_t *ku = kw[e % KD];
         auto k = [&](int w) { return __longlong_as_double((long long)ku[w]); };
         const unsigned slot = (o + a.d[e]) & (RING - 1);
@@ -539,11 +548,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
             double s0 = a0[c], s1 = a1[c];  // |acc| <= q/2 (+ tiny) between diagonals
 #pragma unroll
             for (int j = 0; j < NDIG; j++) {
-#ifdef GW_EXP_NOLDS  // (timing experiment: no ring reads)
-              const double yv = (double)(sl + j + c);
-#else
               const double yv = ring[c][slot][j][sl].d;
-#endif
               if (j == 2) {  // three digits: fold before the third product
                 s0 = f64_red(s0, q, qinv);
                 s1 = f64_red(s1, q, qinv);
@@ -659,16 +664,25 @@ __global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
       store_src(ob + dmax + wv);
     }
     __syncthreads();
-    if (adv + 1 < nadv)
-      load_src(ob + 16 + dmax + wv);
+    const bool more = adv + 1 < nadv;
+    const int e_src = min(GW_SRC_AT, E - 1);
     const unsigned o = ob + wv;
     const uint32_t *tr = tabo + (o & (P - 1)) * 32;
     const size_t koff = ((size_t)tr[16] << 6) + L;
-    // the accumulator words this advance updates, requested before its products
+    // the accumulator words this advance updates and the next advance's new
+    // block: requested at diagonal e_src, behind the first key words (as in
+    // gemv_win_kernel)
     uint64_t av[C];
+    auto load_acc = [&]() {
 #pragma unroll
-    for (int c = 0; c < C; c++)
-      av[c] = (unsigned)c < nc ? a.acc[(size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff] : 0;
+      for (int c = 0; c < C; c++)
+        av[c] = (unsigned)c < nc ? a.acc[(size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff] : 0;
+    };
+    if (GW_SRC_AT < 0) {
+      if (more)
+        load_src(ob + 16 + dmax + wv);
+      load_acc();
+    }
     double f[C];
     uint64_t u[C];
 #pragma unroll
@@ -686,6 +700,11 @@ __global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
       if (e < E) {
         if (e + KD - 1 < W && e + KD - 1 < E)
           kd[(e + KD - 1) % KD] = Kpt[((size_t)(e + KD - 1) << logn) + koff];
+        if (GW_SRC_AT >= 0 && e == e_src) {
+          if (more)
+            load_src(ob + 16 + dmax + wv);
+          load_acc();
+        }
         const uint64_t kw = kd[e % KD];
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
