@@ -61,6 +61,11 @@ PARAMS = {
     # one digit of 5 limbs (alpha > 4: the single-target ks_cols_kernel and the
     # streaming ks_rows_kernel), n=2^13, L=5, dnum=1, K=4 (P 240 > 200 bits)
     "a5": ("params", dict(logn=13, nlimbs=5, nspecial=4, dnum=1, slots=64, q0_bits=40, qi_bits=40, p_bits=60)),
+    # the headline shape with a 60-bit q0 (HECTR's q = 2^109 = q0 q1 at
+    # Delta = 2^50, reference src/ctr.c:514-517) and special primes below 2^51:
+    # three digits of 3/3/2 limbs (60 + 100 bits) under P = 4 x 51 bits, so only
+    # q0 takes the integer forms
+    "m60": ("params", dict(logn=16, nlimbs=8, nspecial=4, dnum=3, slots=64, q0_bits=60, qi_bits=50, p_bits=51)),
 }
 
 
@@ -253,7 +258,7 @@ def mul_batch_both(oracle, product, name, cnt, lvl=None, seeds=(1, 2)):
 
 
 @pytest.mark.parametrize("name", ["bench", "bench_d2", "bench51", "c5", "c5f", "c17", "c14", "c15", "f13", "f15",
-                                  "a5"])
+                                  "a5", "m60"])
 def test_mul_rescale_batch_bitexact(oracle, product, name):
     """Config 3 op at n=2^16, L=8 (dnum=8/K=1 through the streaming inner
     product, the bench's dnum=2/K=4 with 60-bit and with < 2^51 primes), the
@@ -266,7 +271,7 @@ def test_mul_rescale_batch_bitexact(oracle, product, name):
 @pytest.mark.parametrize("name,cnt,chunk", [("bench51", 17, None), ("bench51", 24, None), ("bench_d2", 17, None),
                                             ("bench51", 17, 5), ("bench51", 256, None), ("bench_d2", 256, None),
                                             ("c5", 17, None), ("c5", 64, None), ("c5f", 17, None), ("c5f", 64, None),
-                                            ("c15", 17, None)])
+                                            ("c15", 17, None), ("m60", 17, None)])
 def test_mul_rescale_batch_bench_shape(oracle, product, name, cnt, chunk, monkeypatch):
     """The headline shape (bench.py): n=2^16, L=8,
     dnum=2, K=4 on 17 and 24 pairs (the split key switch's pair ranges of
