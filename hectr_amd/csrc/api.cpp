@@ -2314,67 +2314,19 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const unsigned nsub = g_mul_streams;
   const uint64_t *oend = out + count * out_stride, *aend = a + count * in_stride, *bend = b + count * in_stride;
   const bool alias = (out < aend && a < oend) || (out < bend && b < oend);
-  // (K pipelined sub-chunks with the HBM-bound stages on one stream and the
-  // VALU-bound ones on the other overlapped 39-61 % of the busy time and ran
-  // 2-5 % slower: DESIGN 5b, profiles/r5_ab_pipe.txt, code at 4f1fbb4)
   const bool split2 = count >= 2 && nchunks == 1 && !alias && k_mul_split_ok(lvl) && rlk->reserved &&
                       rlk->dnum == G.dnum;
   const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
   static hipStream_t s2 = nullptr;
-  static hipEvent_t ev_fork, ev_d2, ev_join, eva[8], evb[8];
-  // (experiment: GPQHE_SPLIT_PIPE = K pipelined sub-chunks, HBM-bound stages
-  // on the engine stream, VALU-bound ones on s2; GPQHE_S2_MASK = c keeps the
-  // lowest c bits of every 32-bit word of s2's CU mask clear, so c CUs of
-  // every XCD stay free of the VALU-bound kernels for the HBM-bound ones)
-  static const unsigned pipe = env_u("GPQHE_SPLIT_PIPE", 0), s2mask = env_u("GPQHE_S2_MASK", 0);
-  if (split2 && (nsub == 2 || pipe >= 2) && !s2) {
-    if (s2mask) {
-      uint32_t mv[8];
-      for (unsigned w = 0; w < 8; w++)
-        mv[w] = s2mask >= 32 ? 0u : ~((1u << s2mask) - 1u);
-      HIP_CHECK(hipExtStreamCreateWithCUMask(&s2, 8, mv));
-    } else {
-      HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-    }
+  static hipEvent_t ev_fork, ev_d2, ev_join;
+  // (K pipelined sub-chunks with the HBM-bound stages on one stream and the
+  // VALU-bound ones on the other, with or without a CU mask on the second:
+  // DESIGN 5b, profiles/r5_ab_pipe.txt and r5_ab_cumask.txt, code at 7e2495a)
+  if (split2 && nsub == 2 && !s2) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_d2, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-    for (unsigned k = 0; k < 8; k++) {
-      HIP_CHECK(hipEventCreateWithFlags(&eva[k], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&evb[k], hipEventDisableTiming));
-    }
-  }
-  if (split2 && pipe >= 2 && pipe <= 8 && count >= pipe) {
-    std::vector<std::unique_ptr<Ws>> ws;
-    std::vector<size_t> lo(pipe + 1);
-    for (unsigned k = 0; k <= pipe; k++)
-      lo[k] = count * k / pipe;
-    for (unsigned k = 0; k < pipe; k++)
-      ws.emplace_back(new Ws(k_mul_split_ws_words((unsigned)(lo[k + 1] - lo[k]), lvl, true)));
-    const hipStream_t eng = G.stream;
-    HIP_CHECK(hipEventRecord(ev_fork, eng));
-    HIP_CHECK(hipStreamWaitEvent(s2, ev_fork, 0));
-    auto run = [&](unsigned k, int s0, int s1) {
-      const unsigned c = (unsigned)(lo[k + 1] - lo[k]);
-      k_mul_relin_split(out + lo[k] * out_stride, (lvl - 1) * n, a + lo[k] * in_stride, b + lo[k] * in_stride,
-                        in_stride, lvl * n, evkm, c, lvl, true, ws[k]->p, s0, s1);
-    };
-    for (unsigned k = 0; k < pipe; k++) {
-      run(k, 0, 1);
-      HIP_CHECK(hipEventRecord(eva[k], eng));
-    }
-    G.stream = s2;
-    for (unsigned k = 0; k < pipe; k++) {
-      HIP_CHECK(hipStreamWaitEvent(s2, eva[k], 0));
-      run(k, 1, 4);
-      HIP_CHECK(hipEventRecord(evb[k], s2));
-    }
-    G.stream = eng;
-    for (unsigned k = 0; k < pipe; k++) {
-      HIP_CHECK(hipStreamWaitEvent(eng, evb[k], 0));
-      run(k, 4, 5);
-    }
-    return;
   }
   if (nsub == 2 && split2) {
     const unsigned c1 = (unsigned)(count / 2), c2 = (unsigned)(count - c1);
