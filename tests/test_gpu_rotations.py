@@ -149,6 +149,36 @@ def test_gemv_rot_batch(oracle, product, name, slots, cnt, lvl):
         e.free_evks(k[2])
 
 
+@pytest.mark.parametrize("name", ["bench51", "bench_d2"])
+@pytest.mark.parametrize("diags", [(0, 5), (1, 2, 3, 4, 5), (0, 3, 6, 9, 12, 15), (2, 9, 14)])
+def test_gemv_batch_few_diagonals(oracle, product, name, diags):
+    """he_gemv_batch with a handful of non-zero diagonals: launches of fewer
+    than 4 diagonals (the c0 term in the digit kernel) and of 5-6 (its own
+    pass, the next source block requested at the last diagonal), with and
+    without the identity, on FP64 and mixed prime sets, against the oracle and
+    M @ z."""
+    init_slots(oracle, product, name, 16, seed=57)
+    s, n, lvl, cnt = 16, product.n, 8, 5
+    ko, kp = rot_keys(oracle), rot_keys(product)
+    rng = np.random.default_rng(len(diags))
+    zs = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
+    M = rng.uniform(-1, 1, (s, s)) + 1j * rng.uniform(-1, 1, (s, s))
+    M *= np.isin(np.add.outer(-np.arange(s), np.arange(s)) % s, diags)
+    Mc = np.ascontiguousarray(M.ravel(), dtype=np.complex128)
+    host = encrypt_batch(product, kp[0], zs, nlimbs=lvl)
+    want, got = run_batch(oracle, product, ko[2], kp[2], "he_gemv_batch", host, cnt * 2 * (lvl - 1) * n,
+                          Mc.ctypes.data, "IN", cnt, lvl)
+    assert np.array_equal(got, want), f"gemv: {np.count_nonzero(got != want)} residues differ"
+    sk, delta = kp[1], product.info.delta
+    ct = product.ct()
+    product.import_(ct, got.reshape(cnt, -1)[cnt - 1], lvl - 1, scale=delta)
+    dz = product.decrypt(ct, sk)
+    product.free(ct)
+    assert np.abs(dz - M @ zs[cnt - 1]).max() < 1e-6 * max(1.0, np.abs(M @ zs[cnt - 1]).max())
+    for e, k in ((oracle, ko), (product, kp)):
+        e.free_evks(k[2])
+
+
 def test_gemv_rot_batch_chunks_and_empty(oracle, product, monkeypatch):
     """The batch path's chunk loop (GPQHE_GEMV_CHUNK=2: 5 ciphertexts as
     2 + 2 + 1, the workspace and orbit table per chunk) against the oracle, and
