@@ -312,9 +312,10 @@ struct GwAcc3 {
 // three digits (a fourth ring word costs one ciphertext per workgroup, 3 -> 2,
 // against a separate pass that measured slower there) and for launches of a
 // few diagonals (a rotation: the separate pass's fixed cost).
-#ifndef GW_SRC_AT
-#define GW_SRC_AT 8
-#endif
+// the diagonal at which an advance requests the next advance's source block
+// (and the c0 pass its accumulator words): 8 against before diagonal 0 (the
+// round-5 A/B, profiles/r5_ab_gemv_srcat.json: 4 and 12 within noise of 8)
+constexpr int GW_SRC_AT = 8;
 template <int NDIG, int W, bool INT, bool SPLIT = false, bool C0IN = false>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
@@ -402,8 +403,6 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     // wave of the workgroup would wait out its HBM latency together
     const bool more = adv + 1 < nadv;
     const int e_src = min(GW_SRC_AT, E - 1);
-    if (GW_SRC_AT < 0 && more)
-      load_src(ob + 16 + dmax + wv);
     const unsigned o = ob + wv;
     const uint32_t *tr = tabo + (o & (P - 1)) * 32;
     const size_t koff = ((size_t)tr[16] << 6) + L;
@@ -437,7 +436,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
           kc[w] = kn[w];
         if (e + 1 < E)
           load_keys(e + 1, kn);
-        if (GW_SRC_AT >= 0 && e == e_src && more)
+        if (e == e_src && more)
           load_src(ob + 16 + dmax + wv);
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
@@ -526,7 +525,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       if (!INT && e < E) {
         if (e + KD - 1 < W && e + KD - 1 < E)
           load_keys(e + KD - 1);
-        if (GW_SRC_AT >= 0 && e == e_src && more)
+        if (e == e_src && more)
           load_src(ob + 16 + dmax + wv);
         const uint64_t *ku = kw[e % KD];
         auto k = [&](int w) { return __longlong_as_double((long long)ku[w]); };
@@ -678,11 +677,6 @@ __global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
       for (int c = 0; c < C; c++)
         av[c] = (unsigned)c < nc ? a.acc[(size_t)(p0 + c) * a.acc_stride + ((size_t)t << logn) + koff] : 0;
     };
-    if (GW_SRC_AT < 0) {
-      if (more)
-        load_src(ob + 16 + dmax + wv);
-      load_acc();
-    }
     double f[C];
     uint64_t u[C];
 #pragma unroll
@@ -700,7 +694,7 @@ __global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
       if (e < E) {
         if (e + KD - 1 < W && e + KD - 1 < E)
           kd[(e + KD - 1) % KD] = Kpt[((size_t)(e + KD - 1) << logn) + koff];
-        if (GW_SRC_AT >= 0 && e == e_src) {
+        if (e == e_src) {
           if (more)
             load_src(ob + 16 + dmax + wv);
           load_acc();
