@@ -406,6 +406,9 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     const unsigned o = ob + wv;
     const uint32_t *tr = tabo + (o & (P - 1)) * 32;
     const size_t koff = ((size_t)tr[16] << 6) + L;
+    // the identity's [P pt_0] word, requested before the first key words (at
+    // its use it would wait out its own latency and every load before it)
+    const uint64_t kpid = ident && qs ? ((const uint64_t *)Kpid)[koff] : 0;
     // accumulators: |.| <= q/2 (+ tiny) between diagonals (FP64), [0, 2q) (INT)
     double a0[C], a1[C];
     uint64_t u0[C], u1[C];
@@ -442,7 +445,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
         if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots (c0 here only with C0IN)
           if (qs) {
-            const uint64_t kpi = ((const uint64_t *)Kpid)[koff];
+            const uint64_t kpi = kpid;
 #pragma unroll
             for (int c = 0; c < C; c++) {
               const uint64_t y1 = ring[c][slot][jo][sl].u;
@@ -533,7 +536,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         const unsigned sl = gw_brev((tr[e] + gj[e]) & 63, 6);  // the lane of this output's source
         if (ident && e == 0) {  // the identity: [P pt_0] (c0 with C0IN, c1) on q slots
           if (qs) {
-            const double kpi = Kpid[koff];
+            const double kpi = __longlong_as_double((long long)kpid);
 #pragma unroll
             for (int c = 0; c < C; c++) {
               a1[c] = f64_mulmod_h(ring[c][slot][jo][sl].d, kpi, q, qinv);
