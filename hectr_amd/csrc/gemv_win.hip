@@ -316,7 +316,12 @@ struct GwAcc3 {
 // (and the c0 pass its accumulator words): 8 against before diagonal 0 (the
 // round-5 A/B, profiles/r5_ab_gemv_srcat.json: 4 and 12 within noise of 8)
 constexpr int GW_SRC_AT = 8;
-template <int NDIG, int W, bool INT, bool SPLIT = false, bool C0IN = false>
+// KF (launches of 8 diagonals and more): the FP64 key words are requested on
+// every path of the unrolled diagonal loop (past E at the last diagonal's
+// address); else under each diagonal's branch, where the compiler's wait
+// counts at the joins turn conservative but a launch of a few diagonals (a
+// rotation) does not request 16 diagonals' words
+template <int NDIG, int W, bool INT, bool SPLIT = false, bool C0IN = false, bool KF = false>
 __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
 {
   constexpr int C = gw_cts<NDIG, C0IN>(), RING = 32, NWD = NDIG + (C0IN ? 1 : 0), KW = 2 * NDIG;
@@ -506,8 +511,8 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     // a diagonal's keys overlaps the two before it
     constexpr int KD = 3;
     uint64_t kw[KD][KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
-    auto load_keys = [&](int e) {
-      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
+    auto load_keys = [&](int e, int ea) {  // set e % KD <- diagonal ea's words
+      const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)ea) << logn) + koff) * KW);
 #pragma unroll
       for (int w = 0; w < KW / 2; w++) {
         const ulonglong2 v = kp[w];
@@ -515,19 +520,26 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         kw[e % KD][2 * w + 1] = v.y;
       }
       if constexpr (C0IN) {  // (P slots: zero -- the product below adds nothing)
-        const uint64_t v = ((const uint64_t *)Kpid)[((size_t)e << logn) + koff];
+        const uint64_t v = ((const uint64_t *)Kpid)[((size_t)ea << logn) + koff];
         kw[e % KD][KW] = qs ? v : 0;
       }
     };
+    // (KF: key words requested on every path, past E at the last diagonal's:
+    // a load under the diagonal's branch left the compiler's wait counts
+    // conservative at the joins, a full vmcnt(0) after it)
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
-      if (!INT && e < E)
-        load_keys(e);
+      if (!INT && (KF || e < E))
+        load_keys(e, KF ? min(e, E - 1) : e);
 #pragma unroll
     for (int e = 0; e < W; e++) {
+      if constexpr (KF)
+        if (!INT && e + KD - 1 < W)
+          load_keys(e + KD - 1, min(e + KD - 1, E - 1));
       if (!INT && e < E) {
-        if (e + KD - 1 < W && e + KD - 1 < E)
-          load_keys(e + KD - 1);
+        if constexpr (!KF)
+          if (e + KD - 1 < W && e + KD - 1 < E)
+            load_keys(e + KD - 1, e + KD - 1);
         if (e == e_src && more)
           load_src(ob + 16 + dmax + wv);
         const uint64_t *ku = kw[e % KD];
@@ -687,16 +699,18 @@ __global__ void __launch_bounds__(1024) gemv_c0_kernel(GemvWin a)
       f[c] = 0.0;
       u[c] = 0;
     }
+    // (key words requested on every path, past E at the last diagonal's:
+    // loads under the diagonal's branch left the compiler's wait counts
+    // conservative at the joins -- a full vmcnt(0) after each)
     uint64_t kd[KD];
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
-      if (e < E)
-        kd[e] = Kpt[((size_t)e << logn) + koff];
+      kd[e] = Kpt[((size_t)min(e, E - 1) << logn) + koff];
 #pragma unroll
     for (int e = 0; e < W; e++) {
+      if (e + KD - 1 < W)
+        kd[(e + KD - 1) % KD] = Kpt[((size_t)min(e + KD - 1, E - 1) << logn) + koff];
       if (e < E) {
-        if (e + KD - 1 < W && e + KD - 1 < E)
-          kd[(e + KD - 1) % KD] = Kpt[((size_t)(e + KD - 1) << logn) + koff];
         if (e == e_src) {
           if (more)
             load_src(ob + 16 + dmax + wv);
@@ -984,19 +998,24 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
         setup(c);
         const dim3 grid(xcd_blocks((cnt + cpw - 1) / cpw, c.ns * 2 * nseg));
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(1024), 0, G.stream, c); };
+        // (KF: the FP64 forms of launches of 8 diagonals and more)
         auto form = [&](auto c0) {
           constexpr bool C0 = decltype(c0)::value;
           switch (ndig * 2 + ic) {
-          case 2: go(gemv_win_kernel<1, 16, false, false, C0>); break;
+          case 2:
+            c.E >= 8 ? go(gemv_win_kernel<1, 16, false, false, C0, true>) : go(gemv_win_kernel<1, 16, false, false, C0>);
+            break;
           case 3: split ? go(gemv_win_kernel<1, 16, true, true, C0>) : go(gemv_win_kernel<1, 16, true, false, C0>); break;
-          case 4: go(gemv_win_kernel<2, 16, false, false, C0>); break;
+          case 4:
+            c.E >= 8 ? go(gemv_win_kernel<2, 16, false, false, C0, true>) : go(gemv_win_kernel<2, 16, false, false, C0>);
+            break;
           case 5: split ? go(gemv_win_kernel<2, 16, true, true, C0>) : go(gemv_win_kernel<2, 16, true, false, C0>); break;
           default: break;
           }
         };
         if (ndig >= 3) {  // (always C0IN)
           if (!ic)
-            go(gemv_win_kernel<3, 16, false, false, true>);
+            c.E >= 8 ? go(gemv_win_kernel<3, 16, false, false, true, true>) : go(gemv_win_kernel<3, 16, false, false, true>);
           else if (split)
             go(gemv_win_kernel<3, 16, true, true, true>);
           else
