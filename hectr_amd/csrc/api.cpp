@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <list>
 #include <map>
 #include <memory>
 #include <string>
@@ -30,6 +31,7 @@ static size_t pool_round(size_t b)
 }
 
 static void flush_ew();
+static void fold_cache_trim();
 
 void *pool_alloc(size_t bytes)
 {
@@ -44,9 +46,11 @@ void *pool_alloc(size_t bytes)
   hipError_t e = hipMalloc(&p, b);
   if (e != hipSuccess) {
     // give cached blocks back and retry once (queued elementwise ops may
-    // still name a free-listed block: they run first)
+    // still name a free-listed block: they run first); folded key sets no
+    // running call reads go back too
     flush_ew();
     HIP_CHECK(hipStreamSynchronize(G.stream));
+    fold_cache_trim();
     for (auto &kv : g_free)
       for (void *q : kv.second) {
         (void)hipFree(q);
@@ -99,9 +103,18 @@ struct FoldEntry {
   double *K;
   size_t bytes;
 };
-static std::vector<FoldEntry> g_folds;
+// (a list: a caller's reference to its entry survives the eviction of others)
+static std::list<FoldEntry> g_folds;
+static const double *g_fold_inuse = nullptr;  // the set a running call reads
+// While a call reads a folded set, an out-of-memory retry inside it keeps
+// that set (fold_cache_trim).
+struct FoldUse {
+  explicit FoldUse(const FoldEntry &f) { g_fold_inuse = f.K; }
+  ~FoldUse() { g_fold_inuse = nullptr; }
+};
 
 static void fold_cache_clear();
+static bool gemv_fold_fits(const double *Md, unsigned lvl, const he_evk_t rk[]);
 static bool gemv_win_on(unsigned lvl);
 static const FoldEntry &gemv_fold(const double *Md, unsigned lvl, const he_evk_t rk[]);
 static const FoldEntry &rot_fold(unsigned r, unsigned lvl, const he_evk_t rk[]);
@@ -155,6 +168,16 @@ static void stage_done(Stage &s) { HIP_CHECK(hipEventRecord(s.ev, G.stream)); }
 
 static void *g_zpin = nullptr;  // pinned decode output (he_dcd_ex)
 static size_t g_zpin_bytes = 0;
+
+// he_mul_rescale_batch's second sub-chunk stream and its fork / join events
+// (created on first use, released by hectx_exit: no HIP object of the engine
+// is left for the runtime's or a profiler's exit handlers)
+struct SecondStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, d2 = nullptr, join = nullptr;
+};
+static SecondStream g_s2;
+static hipEvent_t g_dcd_ev = nullptr;  // end of the small-N decode (spec_launch)
 
 static void stage_release()
 {
@@ -745,6 +768,22 @@ extern "C" void hectx_exit(void)
   hp_report();
   check_ctx();
   HIP_CHECK(hipStreamSynchronize(G.stream));
+  // every HIP object the engine created goes here, after its last use: the
+  // second sub-chunk stream and its events, the decode event, the profiling
+  // events and (below, with the pool) the context's own stream
+  if (g_s2.s) {
+    HIP_CHECK(hipStreamSynchronize(g_s2.s));
+    HIP_CHECK(hipEventDestroy(g_s2.fork));
+    HIP_CHECK(hipEventDestroy(g_s2.d2));
+    HIP_CHECK(hipEventDestroy(g_s2.join));
+    HIP_CHECK(hipStreamDestroy(g_s2.s));
+    g_s2 = SecondStream{};
+  }
+  if (g_dcd_ev) {
+    HIP_CHECK(hipEventDestroy(g_dcd_ev));
+    g_dcd_ev = nullptr;
+  }
+  k_prof_release();
   gemv_cache_clear();
   fold_cache_clear();
   g_key_gen++;
@@ -759,6 +798,12 @@ extern "C" void hectx_exit(void)
   g_spec_pk1_next = nullptr;
   pool_release_all();
   stage_release();
+  if (G.own_stream) {
+    HIP_CHECK(hipStreamDestroy(G.own_stream));
+    if (G.stream == G.own_stream)
+      G.stream = nullptr;  // (a caller's stream from gpqhe_set_stream stays set)
+    G.own_stream = nullptr;
+  }
   G.init = false;
 }
 
@@ -1238,7 +1283,6 @@ static void *zpin(size_t bytes)
 // After the small-N decode (he_dcd_ex): record the decode's end, then launch
 // the next step's encryption noise (SpecNoise) if the last flush had one run
 // of encryptions.  True if launched (the caller then waits on g_dcd_ev).
-static hipEvent_t g_dcd_ev = nullptr;
 static bool spec_launch()
 {
   static const bool on = env_u("GPQHE_SPEC", 1) != 0;
@@ -1816,6 +1860,7 @@ extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const 
   const he_evk_t *k = find_rot_key(rk, rot, g);
   if (gemv_win_on(lvl)) {  // (reads every input word before the ModDown writes out: in place is fine)
     const FoldEntry &f = rot_fold(rot, lvl, rk);
+    FoldUse use(f);
     const double scale = in->scale;
     k_gemv_batch_ex(out->data, 0, pstride(out), in->data, 0, pstride(in), 1, lvl, f.K, f.d.data(), 1, 0);
     out->nlimbs = lvl;
@@ -2098,12 +2143,19 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   if (lvl < 2)
     gpqhe_die("he_gemv: input at the lowest level");
   const double *Md = (const double *)M;
-  if (gemv_win_on(lvl)) {  // n >= 2^13, FP64 prime sets: the windowed batch path, one ciphertext
+  // n >= 2^13: the windowed batch path on one ciphertext, unqueued.  It takes
+  // no part in the small-N step's queues and speculation (check_ctx drops
+  // any pending speculative ModUp): those serve HECTR's own ring (n <= 2^12),
+  // where a step is a handful of small launches; at 2^13 and above a gemv is
+  // tens of microseconds of device work on its own.  (In place, y == x, is
+  // fine: every input word is read before the ModDown writes y.)
+  if (gemv_win_on(lvl) && gemv_fold_fits(Md, lvl, rk)) {
     if (lazy)
       flush_ew();
     check_ctx();
     prov_forget(y->data, pstride(y));
     const FoldEntry &f = gemv_fold(Md, lvl, rk);
+    FoldUse use(f);
     const double scale = x->scale;
     k_gemv_batch_ex(y->data, 0, pstride(y), x->data, 0, pstride(x), 1, lvl, f.K, f.d.data(), (unsigned)f.d.size(), 1);
     y->nlimbs = lvl - 1;
@@ -2317,17 +2369,17 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
   const bool split2 = count >= 2 && nchunks == 1 && !alias && k_mul_split_ok(lvl) && rlk->reserved &&
                       rlk->dnum == G.dnum;
   const uint64_t *evkm = (const uint64_t *)(uintptr_t)rlk->reserved;
-  static hipStream_t s2 = nullptr;
-  static hipEvent_t ev_fork, ev_d2, ev_join;
   // (K pipelined sub-chunks with the HBM-bound stages on one stream and the
   // VALU-bound ones on the other, with or without a CU mask on the second:
   // DESIGN 5b, profiles/r5_ab_pipe.txt and r5_ab_cumask.txt, code at 7e2495a)
-  if (split2 && nsub == 2 && !s2) {
-    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_d2, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  if (split2 && nsub == 2 && !g_s2.s) {
+    HIP_CHECK(hipStreamCreateWithFlags(&g_s2.s, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&g_s2.fork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&g_s2.d2, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&g_s2.join, hipEventDisableTiming));
   }
+  hipStream_t s2 = g_s2.s;
+  hipEvent_t ev_fork = g_s2.fork, ev_d2 = g_s2.d2, ev_join = g_s2.join;
   if (nsub == 2 && split2) {
     const unsigned c1 = (unsigned)(count / 2), c2 = (unsigned)(count - c1);
     // both workspaces come from the engine stream's pool before the fork and
@@ -2359,12 +2411,23 @@ extern "C" void he_mul_rescale_batch(uint64_t *out, const uint64_t *a, const uin
 }
 
 // ---------------------------------------------------------------------------
-// he_gemv / he_rot on the windowed FP64 path (gemv_win.hip) for n >= 2^13 and
-// prime sets below 2^51.  The rotation keys are folded with their diagonals
-// once and cached: HECTR passes the same gain matrices every control step
-// (src/hempc.c:232-238), the bench the same matrix every step.  Any change of
-// a key (generation, import, free) drops every folded set (g_key_gen).
+// he_gemv / he_rot on the windowed path (gemv_win.hip) for n >= 2^13.  The
+// rotation keys are folded with their diagonals once and cached: HECTR passes
+// the same gain matrices every control step (src/hempc.c:232-238), the bench
+// the same matrix every step.  A change of a key (generation, import, free)
+// bumps g_key_gen: entries of an older generation never match again and are
+// released at the next insert (or when the pool runs out of memory).
+// A matrix whose folded set would exceed the cap (GPQHE_FOLD_MIB, 16 GiB:
+// (2 ndig nm + lvl) n words per non-zero diagonal, ~30 GB for a dense
+// 1024-slot matrix at N=2^16, L=8) takes the per-ciphertext path, whose
+// diagonal cache is bounded and streams.
 // ---------------------------------------------------------------------------
+static size_t fold_cap()
+{
+  static const size_t cap = (size_t)env_u("GPQHE_FOLD_MIB", 16384) << 20;
+  return cap;
+}
+
 static void fold_cache_clear()
 {
   for (FoldEntry &f : g_folds)
@@ -2372,17 +2435,35 @@ static void fold_cache_clear()
   g_folds.clear();
 }
 
+// out of memory: every set no running call reads goes back to the pool
+static void fold_cache_trim()
+{
+  for (auto it = g_folds.begin(); it != g_folds.end();)
+    if (it->K != g_fold_inuse) {
+      pool_free(it->K);
+      it = g_folds.erase(it);
+    } else {
+      ++it;
+    }
+}
+
 static const FoldEntry &fold_insert(FoldEntry &&f)
 {
-  // a few sets (a 16-slot gemv at N=2^16, L=8 folds to 480 MB)
-  static const size_t cap = (size_t)env_u("GPQHE_FOLD_MIB", 16384) << 20;
+  // a few sets (a 16-slot gemv at N=2^16, L=8 folds to 480 MB); f.bytes is
+  // within the cap (gemv_fold_fits)
   size_t total = f.bytes;
-  for (const FoldEntry &e : g_folds)
-    total += e.bytes;
-  while (!g_folds.empty() && (g_folds.size() >= 8 || total > cap)) {
+  for (auto it = g_folds.begin(); it != g_folds.end();)
+    if (it->gen != g_key_gen) {  // folded with keys that changed since
+      pool_free(it->K);
+      it = g_folds.erase(it);
+    } else {
+      total += it->bytes;
+      ++it;
+    }
+  while (!g_folds.empty() && (g_folds.size() >= 8 || total > fold_cap())) {
     total -= g_folds.front().bytes;
     pool_free(g_folds.front().K);
-    g_folds.erase(g_folds.begin());
+    g_folds.pop_front();
   }
   g_folds.push_back(std::move(f));
   return g_folds.back();
@@ -2394,33 +2475,63 @@ static bool gemv_win_on(unsigned lvl)
   return on && k_gemv_win_ok(lvl);
 }
 
-// The non-zero diagonals of M, encoded at scale q_{lvl-1} over basis_qp(lvl),
-// folded with their rotation keys.
-static const FoldEntry &gemv_fold(const double *Md, unsigned lvl, const he_evk_t rk[])
+// The rotations of M's non-zero diagonals, and (diags) the diagonals
+// themselves, slots complex values each.
+static std::vector<unsigned> gemv_diagonals(const double *Md, std::vector<double> *diags)
+{
+  const unsigned s = G.slots;
+  std::vector<unsigned> ds;
+  for (unsigned d = 0; d < s; d++) {
+    bool nz = false;
+    for (unsigned i = 0; i < s && !nz; i++) {
+      const size_t src = (size_t)i * s + (i + d) % s;
+      nz = Md[2 * src] != 0.0 || Md[2 * src + 1] != 0.0;
+    }
+    if (!nz)
+      continue;
+    ds.push_back(d);
+    if (diags)
+      for (unsigned i = 0; i < s; i++) {
+        const size_t src = (size_t)i * s + (i + d) % s;
+        diags->push_back(Md[2 * src]);
+        diags->push_back(Md[2 * src + 1]);
+      }
+  }
+  return ds;
+}
+
+static const FoldEntry *fold_find(const double *Md, unsigned lvl, const he_evk_t rk[])
 {
   const unsigned s = G.slots;
   const size_t mwords = 2 * (size_t)s * s;
   for (const FoldEntry &f : g_folds)
     if (!f.M.empty() && f.s == s && f.lvl == lvl && f.gen == g_key_gen && f.rk == rk &&
         !memcmp(f.M.data(), Md, mwords * 8))
-      return f;
-  std::vector<unsigned> ds;
+      return &f;
+  return nullptr;
+}
+
+// Would M's folded set (plus the encoded diagonals it is folded from) fit the
+// cap?  Cached sets always do.
+static bool gemv_fold_fits(const double *Md, unsigned lvl, const he_evk_t rk[])
+{
+  if (fold_find(Md, lvl, rk))
+    return true;
+  const size_t E = gemv_diagonals(Md, nullptr).size();
+  const size_t pts = E * (((size_t)lvl + G.K) << G.logn) * 8;
+  return k_gemv_fold_words((unsigned)E, lvl) * 8 + pts <= fold_cap();
+}
+
+// The non-zero diagonals of M, encoded at scale q_{lvl-1} over basis_qp(lvl),
+// folded with their rotation keys (the caller checked gemv_fold_fits).
+static const FoldEntry &gemv_fold(const double *Md, unsigned lvl, const he_evk_t rk[])
+{
+  if (const FoldEntry *f = fold_find(Md, lvl, rk))
+    return *f;
+  const unsigned s = G.slots;
+  const size_t mwords = 2 * (size_t)s * s;
   std::vector<double> diags;
-  for (unsigned d = 0; d < s; d++) {
-    bool nz = false;
-    const size_t at = diags.size();
-    diags.resize(at + 2 * (size_t)s);
-    for (unsigned i = 0; i < s; i++) {
-      const size_t src = (size_t)i * s + (i + d) % s;
-      diags[at + 2 * i] = Md[2 * src];
-      diags[at + 2 * i + 1] = Md[2 * src + 1];
-      nz |= Md[2 * src] != 0.0 || Md[2 * src + 1] != 0.0;
-    }
-    if (nz)
-      ds.push_back(d);
-    else
-      diags.resize(at);
-  }
+  const std::vector<unsigned> ds = gemv_diagonals(Md, &diags);
   const unsigned E = (unsigned)ds.size();
   unsigned mods[GPQHE_MAXMOD];
   const unsigned nm = basis_qp(lvl, mods);
@@ -2454,9 +2565,10 @@ static const FoldEntry &rot_fold(unsigned r, unsigned lvl, const he_evk_t rk[])
 static bool gemv_batch_fast(uint64_t *y, const double *Md, const uint64_t *x, size_t count, unsigned lvl,
                             const he_evk_t rk[])
 {
-  if (!gemv_win_on(lvl))
+  if (!gemv_win_on(lvl) || !gemv_fold_fits(Md, lvl, rk))
     return false;
   const FoldEntry &f = gemv_fold(Md, lvl, rk);
+  FoldUse use(f);
   k_gemv_batch(y, x, count, lvl, f.K, f.d.data(), (unsigned)f.d.size(), 1);
   return true;
 }
@@ -2467,6 +2579,7 @@ static bool rot_batch_fast(uint64_t *out, const uint64_t *x, size_t count, unsig
   if (!gemv_win_on(lvl))
     return false;
   const FoldEntry &f = rot_fold(r, lvl, rk);
+  FoldUse use(f);
   k_gemv_batch(out, x, count, lvl, f.K, f.d.data(), 1, 0);
   return true;
 }

@@ -444,6 +444,7 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
                      unsigned lvl, int mode);
 bool k_prof_on();
+void k_prof_release();
 // Live kernel statistics (gpqhe_prof_enable): HIP events around one launch
 // on the engine stream, per kernel class (names: kernels.hip kc_names).
 enum KClass {

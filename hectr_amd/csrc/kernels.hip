@@ -93,6 +93,19 @@ bool k_prof_on()
   return g_prof;
 }
 
+// hectx_exit: the timing events (pooled and still recorded)
+void k_prof_release()
+{
+  for (const ProfEntry &e : g_prof_entries) {
+    g_ev_pool.push_back(e.a);
+    g_ev_pool.push_back(e.b);
+  }
+  g_prof_entries.clear();
+  for (hipEvent_t e : g_ev_pool)
+    HIP_CHECK(hipEventDestroy(e));
+  g_ev_pool.clear();
+}
+
 extern "C" void gpqhe_prof_enable(int on)
 {
   g_prof = on != 0;

@@ -109,6 +109,25 @@ def test_bench_self_launch_two_ranks():
     assert lines[0]["n_gpus"] == 2 and lines[0]["max_over_ranks"] == 2.0
 
 
+def test_bench_self_launch_eight_ranks():
+    """The driver's 8-GPU command shape without the engine: bench.py --gpus 8
+    starts eight rank processes that meet over gloo (rendezvous on
+    127.0.0.1), run the barrier and the max-over-ranks reduction, and rank 0
+    prints one line with n_gpus = 8 and the largest rank's value."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--launch-check"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 8 and lines[0]["max_over_ranks"] == 8.0
+
+
 def test_bench_rejects_world_mismatch():
     """Under an external launcher, --gpus must equal WORLD_SIZE (a scale run
     must never silently time fewer ranks than it reports)."""

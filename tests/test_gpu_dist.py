@@ -79,3 +79,32 @@ def test_bench_two_ranks_default_legs():
     assert d["config5"]["value"] > 0 and d["config5"]["value_60bit"] > 0 and d["config5"]["hempc_gemv"]["value"] > 0
     g = d["gemv"]
     assert g["value"] > 0 and g["alt_primes"]["value"] > 0 and len(g["rank_times_s"]) == 2
+
+
+@pytest.mark.timeout(900)
+def test_bench_eight_ranks_shards_bit_exact():
+    """Rehearsal of the driver's 8-GPU command shape on the one GPU of the test
+    box: bench.py --gpus 8 starts eight rank processes (gloo for the
+    collectives; every rank on device LOCAL_RANK mod device_count), each runs
+    the headline, config 5, the gemv leg and config 5 as a hempc batch on its
+    one-item shard (the headline's single pair takes the one-stream path),
+    and rank 0 compares every leg's gathered shards with one context's run of
+    the 8-item global batch.  The line carries eight rank times per leg."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HECTR_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--batch", "1", "--steps", "2", "--warmup",
+           "1", "--no-cpu", "--no-cstr", "--no-ntt", "--alt-bits", "0", "--c5-batch", "1", "--gemv-batch", "1",
+           "--c5-gemv-batch", "1", "--check-shards"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=840, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 8 and len(d["rank_times_s"]) == 8
+    assert d["shard_check"]["pairs"] == 8 and d["shard_check"]["bit_exact"], d["shard_check"]
+    c5, g = d["config5"], d["gemv"]
+    assert c5["shard_check"] == {"pairs": 8, "ranks": 8, "bit_exact": True, "differing_pairs": []}, c5["shard_check"]
+    assert g["shard_check"] == {"cts": 8, "ranks": 8, "bit_exact": True, "differing_cts": []}, g["shard_check"]
+    h = c5["hempc_gemv"]
+    assert h["shard_check"] == {"cts": 8, "ranks": 8, "bit_exact": True, "differing_cts": []}, h["shard_check"]
+    assert len(c5["rank_times_s"]) == 8 and len(g["rank_times_s"]) == 8 and len(h["rank_times_s"]) == 8
