@@ -422,12 +422,69 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
       a0[c] = a1[c] = 0.0;
       u0[c] = u1[c] = 0;
     }
-    if constexpr (INT) {
-      // one diagonal at a time (the body is too long to unroll over 16: a
-      // register array indexed by the diagonal would go to scratch); the
-      // next diagonal's key words in flight meanwhile
+    // INT: one diagonal's products (key words ku), the accumulators in [0, 2q)
+    auto int_diag = [&](int e, const uint64_t *ku, unsigned slot, unsigned sl) {
+      if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots (c0 here only with C0IN)
+        if (qs) {
+          const uint64_t kpi = kpid;
+#pragma unroll
+          for (int c = 0; c < C; c++) {
+            const uint64_t y1 = ring[c][slot][jo][sl].u;
+            if constexpr (SPLIT) {
+              GwAcc3 b1;
+              b1.mac(y1, kpi);
+              u1[c] = b1.redc(qi, qni);
+              if constexpr (C0IN) {
+                GwAcc3 b0;
+                b0.mac(ring[c][slot][NDIG][sl].u, kpi);
+                u0[c] = b0.redc(qi, qni);
+              }
+            } else {
+              u1[c] = gw_redc(mulhi64(y1, kpi), y1 * kpi, qi, qni);
+              if constexpr (C0IN) {
+                const uint64_t y0 = ring[c][slot][NDIG][sl].u;
+                u0[c] = gw_redc(mulhi64(y0, kpi), y0 * kpi, qi, qni);
+              }
+            }
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        if constexpr (SPLIT) {
+          GwAcc3 b0, b1;
+#pragma unroll
+          for (int j = 0; j < NDIG; j++) {
+            const uint64_t yv = ring[c][slot][j][sl].u;
+            b0.mac(yv, ku[j]);
+            b1.mac(yv, ku[NDIG + j]);
+          }
+          if (C0IN && qs)
+            b0.mac(ring[c][slot][NWD - 1][sl].u, ku[KW]);
+          u0[c] = lazy_lt2q(u0[c] + b0.redc(qi, qni), q2);
+          u1[c] = lazy_lt2q(u1[c] + b1.redc(qi, qni), q2);
+        } else {
+          uint64_t h0 = 0, l0 = 0, h1 = 0, l1 = 0;
+#pragma unroll
+          for (int j = 0; j < NDIG; j++) {
+            const uint64_t yv = ring[c][slot][j][sl].u;
+            gw_mac128(h0, l0, yv, ku[j]);
+            gw_mac128(h1, l1, yv, ku[NDIG + j]);
+          }
+          if (C0IN && qs)
+            gw_mac128(h0, l0, ring[c][slot][NWD - 1][sl].u, ku[KW]);
+          u0[c] = lazy_lt2q(u0[c] + gw_redc(h0, l0, qi, qni), q2);
+          u1[c] = lazy_lt2q(u1[c] + gw_redc(h1, l1, qi, qni), q2);
+        }
+      }
+    };
+    if constexpr (INT && !KF) {
+      // a launch of a few diagonals (rotations): one diagonal at a time with
+      // the next diagonal's key words in flight (the unrolled form below
+      // spilled 18-64 B/lane for them)
       uint64_t kc[KW + 1], kn[KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
-      auto load_keys = [&](int e, uint64_t (&kk)[KW + 1]) {
+      auto load_keys1 = [&](int e, uint64_t (&kk)[KW + 1]) {
         const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
 #pragma unroll
         for (int w = 0; w < KW / 2; w++) {
@@ -437,74 +494,16 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         }
         kk[KW] = C0IN && qs ? ((const uint64_t *)Kpid)[((size_t)e << logn) + koff] : 0;
       };
-      load_keys(0, kn);
+      load_keys1(0, kn);
       for (int e = 0; e < E; e++) {
 #pragma unroll
         for (int w = 0; w <= KW; w++)
           kc[w] = kn[w];
         if (e + 1 < E)
-          load_keys(e + 1, kn);
+          load_keys1(e + 1, kn);
         if (e == e_src && more)
           load_src(ob + 16 + dmax + wv);
-        const unsigned slot = (o + a.d[e]) & (RING - 1);
-        const unsigned sl = gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6);
-        if (ident && e == 0) {  // the identity: [P pt_0] (c0, c1) on q slots (c0 here only with C0IN)
-          if (qs) {
-            const uint64_t kpi = kpid;
-#pragma unroll
-            for (int c = 0; c < C; c++) {
-              const uint64_t y1 = ring[c][slot][jo][sl].u;
-              if constexpr (SPLIT) {
-                GwAcc3 b1;
-                b1.mac(y1, kpi);
-                u1[c] = b1.redc(qi, qni);
-                if constexpr (C0IN) {
-                  GwAcc3 b0;
-                  b0.mac(ring[c][slot][NDIG][sl].u, kpi);
-                  u0[c] = b0.redc(qi, qni);
-                }
-              } else {
-                u1[c] = gw_redc(mulhi64(y1, kpi), y1 * kpi, qi, qni);
-                if constexpr (C0IN) {
-                  const uint64_t y0 = ring[c][slot][NDIG][sl].u;
-                  u0[c] = gw_redc(mulhi64(y0, kpi), y0 * kpi, qi, qni);
-                }
-              }
-            }
-          }
-          continue;
-        }
-        if constexpr (SPLIT) {
-#pragma unroll
-          for (int c = 0; c < C; c++) {
-            GwAcc3 b0, b1;
-#pragma unroll
-            for (int j = 0; j < NDIG; j++) {
-              const uint64_t yv = ring[c][slot][j][sl].u;
-              b0.mac(yv, kc[j]);
-              b1.mac(yv, kc[NDIG + j]);
-            }
-            if (C0IN && qs)
-              b0.mac(ring[c][slot][NWD - 1][sl].u, kc[KW]);
-            u0[c] = lazy_lt2q(u0[c] + b0.redc(qi, qni), q2);
-            u1[c] = lazy_lt2q(u1[c] + b1.redc(qi, qni), q2);
-          }
-          continue;
-        }
-#pragma unroll
-        for (int c = 0; c < C; c++) {
-          uint64_t h0 = 0, l0 = 0, h1 = 0, l1 = 0;
-#pragma unroll
-          for (int j = 0; j < NDIG; j++) {
-            const uint64_t yv = ring[c][slot][j][sl].u;
-            gw_mac128(h0, l0, yv, kc[j]);
-            gw_mac128(h1, l1, yv, kc[NDIG + j]);
-          }
-          if (C0IN && qs)
-            gw_mac128(h0, l0, ring[c][slot][NWD - 1][sl].u, kc[KW]);
-          u0[c] = lazy_lt2q(u0[c] + gw_redc(h0, l0, qi, qni), q2);
-          u1[c] = lazy_lt2q(u1[c] + gw_redc(h1, l1, qi, qni), q2);
-        }
+        int_diag(e, kc, (o + a.d[e]) & (RING - 1), gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6));
       }
     }
     // key words two diagonals ahead (a ring of three sets): the L2 latency of
@@ -527,16 +526,17 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     // (KF: key words requested on every path, past E at the last diagonal's:
     // a load under the diagonal's branch left the compiler's wait counts
     // conservative at the joins, a full vmcnt(0) after it)
+    constexpr bool UNR = !INT || KF;  // the unrolled loop below runs this launch
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
-      if (!INT && (KF || e < E))
+      if (UNR && (KF || e < E))
         load_keys(e, KF ? min(e, E - 1) : e);
 #pragma unroll
     for (int e = 0; e < W; e++) {
       if constexpr (KF)
-        if (!INT && e + KD - 1 < W)
+        if (e + KD - 1 < W)
           load_keys(e + KD - 1, min(e + KD - 1, E - 1));
-      if (!INT && e < E) {
+      if (UNR && e < E) {
         if constexpr (!KF)
           if (e + KD - 1 < W && e + KD - 1 < E)
             load_keys(e + KD - 1, e + KD - 1);
@@ -546,7 +546,9 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         auto k = [&](int w) { return __longlong_as_double((long long)ku[w]); };
         const unsigned slot = (o + a.d[e]) & (RING - 1);
         const unsigned sl = gw_brev((tr[e] + gj[e]) & 63, 6);  // the lane of this output's source
-        if (ident && e == 0) {  // the identity: [P pt_0] (c0 with C0IN, c1) on q slots
+        if constexpr (INT) {
+          int_diag(e, ku, slot, sl);
+        } else if (ident && e == 0) {  // the identity: [P pt_0] (c0 with C0IN, c1) on q slots
           if (qs) {
             const double kpi = __longlong_as_double((long long)kpid);
 #pragma unroll
@@ -1005,11 +1007,21 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
           case 2:
             c.E >= 8 ? go(gemv_win_kernel<1, 16, false, false, C0, true>) : go(gemv_win_kernel<1, 16, false, false, C0>);
             break;
-          case 3: split ? go(gemv_win_kernel<1, 16, true, true, C0>) : go(gemv_win_kernel<1, 16, true, false, C0>); break;
+          case 3:
+            if (split)
+              !C0 && c.E >= 8 ? go(gemv_win_kernel<1, 16, true, true, false, true>) : go(gemv_win_kernel<1, 16, true, true, C0>);
+            else
+              !C0 && c.E >= 8 ? go(gemv_win_kernel<1, 16, true, false, false, true>) : go(gemv_win_kernel<1, 16, true, false, C0>);
+            break;
           case 4:
             c.E >= 8 ? go(gemv_win_kernel<2, 16, false, false, C0, true>) : go(gemv_win_kernel<2, 16, false, false, C0>);
             break;
-          case 5: split ? go(gemv_win_kernel<2, 16, true, true, C0>) : go(gemv_win_kernel<2, 16, true, false, C0>); break;
+          case 5:
+            if (split)
+              !C0 && c.E >= 8 ? go(gemv_win_kernel<2, 16, true, true, false, true>) : go(gemv_win_kernel<2, 16, true, true, C0>);
+            else
+              !C0 && c.E >= 8 ? go(gemv_win_kernel<2, 16, true, false, false, true>) : go(gemv_win_kernel<2, 16, true, false, C0>);
+            break;
           default: break;
           }
         };
@@ -1017,9 +1029,9 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
           if (!ic)
             c.E >= 8 ? go(gemv_win_kernel<3, 16, false, false, true, true>) : go(gemv_win_kernel<3, 16, false, false, true>);
           else if (split)
-            go(gemv_win_kernel<3, 16, true, true, true>);
+            c.E >= 8 ? go(gemv_win_kernel<3, 16, true, true, true, true>) : go(gemv_win_kernel<3, 16, true, true, true>);
           else
-            go(gemv_win_kernel<3, 16, true, false, true>);
+            c.E >= 8 ? go(gemv_win_kernel<3, 16, true, false, true, true>) : go(gemv_win_kernel<3, 16, true, false, true>);
         } else if (c0in) {
           form(std::true_type{});
         } else {

@@ -37,6 +37,9 @@
 #ifndef KSQ_SPLIT_AR
 #define KSQ_SPLIT_AR 1
 #endif
+#ifndef KSQ_SCALAR_Q
+#define KSQ_SCALAR_Q 1
+#endif
 #ifndef KSQ_C5_DROP_LTW
 #define KSQ_C5_DROP_LTW 2
 #endif
@@ -75,6 +78,31 @@
 // lines; loads one phase ahead in the kept slots' kernel -- 1868 -> 1960 /
 // 2215 us, spills; one kernel per lazy-reduction policy with the slots
 // launched in runs of one policy -- keep 1869, drop 1213 us.  DESIGN 5b.)
+
+// A wave-uniform pointer pinned to SGPRs where it is used: the compiler
+// otherwise hoists (uniform base + lane offset) out of the pair loop as 64-bit
+// VGPR pairs, one per stream, and spills them (each reload's vmcnt(0) then
+// also waits out the prefetches in flight).  The pointer must be uniform.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <class P>
+using gptr = __attribute__((address_space(1))) P *;  // a global-memory pointer
+template <class P>
+__device__ __forceinline__ gptr<P> sgpr_ptr(P *p)
+{
+#if KSQ_SCALAR_Q
+  // (readfirstlane: an opaque scalar; the cast back to the global address
+  // space keeps global_load / global_store, not flat, instructions)
+  // (the builtin returns int: each half goes through uint32_t, or the low
+  // one would be sign-extended into the high one)
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint64_t s = ((uint64_t)hi << 32) | lo;
+  return (gptr<P>)(P *)(uintptr_t)s;
+#else
+  return (gptr<P>)p;
+#endif
+}
 
 // the policy with its lazy-reduction choice fixed (LZ 0 / 1; -1 as it is)
 template <int LZ>
@@ -131,6 +159,10 @@ __global__ void __launch_bounds__(256 * QN, 1)
   const size_t toff = (size_t)row0 << LOGN2;
   const bool f64 = ALLF || (AR == 0 && q < F64_QMAX && tw.fwdd);  // key words as plain doubles (to_mont_kernel)
   const uint64_t sk = ksc[t];  // the folded ModDown factor of this slot
+  // [P s_t]_t and its Shoup companion, read before any store of the kernel
+  // (a uniform load a store may clobber is a vector load, and its wait,
+  // vmcnt(0), also waited out every prefetch in flight)
+  const uint64_t kp0 = KEEP ? kps[2 * t] : 0, kp1 = KEEP ? kps[2 * t + 1] : 0;
   for (unsigned idx = threadIdx.x; idx < 2 * NDIG * 2048; idx += 256 * QN) {
     const unsigned c = idx >> 11, w = idx & 2047;
     // plain (FP64 moduli) or Montgomery form: either way x s_t stays in its form
@@ -138,16 +170,27 @@ __global__ void __launch_bounds__(256 * QN, 1)
     kl[c][w] = f64 ? (uint64_t)__double_as_longlong((double)e) : e;
   }
   __syncthreads();
-  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  // the quarter (pair stream) is wave-uniform: as a scalar, the pair index,
+  // the loop bound tests and the streams' base addresses live in SGPRs (no
+  // exec-masked pair loop, 32-bit lane offsets)
+#if KSQ_SCALAR_Q
+  const int qi = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+#else
+  const int qi = threadIdx.x >> 8;
+#endif
+  const int th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  // this lane's word offset in a row tile (32-bit, so a uniform base in SGPRs
+  // plus it is one global access with a scalar base)
+  const unsigned lo = (unsigned)((row << LOGN2) + l);
   uint64_t *lq = rt[qi];
   const unsigned jo = t < lvl ? t / alpha : NDIG;  // the digit owning q limb t (none on P limbs)
   const int nx = jo < NDIG ? NDIG - 1 : NDIG;
   auto jof = [&](int u) -> unsigned { return (unsigned)u < jo ? (unsigned)u : (unsigned)u + 1; };
   auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
-    const uint64_t *s = T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff;
+    gptr<const uint64_t> s = sgpr_ptr(T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      x[k] = s[(row << LOGN2) + l + T::TA * k];
+      x[k] = s[lo + T::TA * k];
   };
   unsigned p = pb0 + qi;
   uint64_t xn[NX > 0 ? NX : 1][8];
@@ -206,16 +249,17 @@ __global__ void __launch_bounds__(256 * QN, 1)
         }
       // the dropped q slot's first half of input words is requested here, so
       // its latency overlaps the converted limb's row pass (1037 -> 1018 us)
-      const size_t ioff = p * d01.in_stride + ((size_t)t << logn) + toff + 8 * th;
-      const uint64_t *pin[4] = {d01.a + ioff, d01.b + ioff, d01.a + ioff + d01.in_pstride,
-                                d01.b + ioff + d01.in_pstride};  // a0, b0, a1, b1
+      const size_t ioff = p * d01.in_stride + ((size_t)t << logn) + toff;  // (uniform)
+      gptr<const uint64_t> pin[4] = {sgpr_ptr(d01.a + ioff), sgpr_ptr(d01.b + ioff), sgpr_ptr(d01.a + ioff + d01.in_pstride),
+                                sgpr_ptr(d01.b + ioff + d01.in_pstride)};  // a0, b0, a1, b1
+      const unsigned lin = 8u * (unsigned)th;
       uint64_t inw[4][4];
       auto ld_in = [&](int h) {
 #pragma unroll
         for (int a = 0; a < 4; a++) {
-          const ulonglong2 *v2 = (const ulonglong2 *)(pin[a] + 4 * h);
-          const ulonglong2 w0 = v2[0];
-          const ulonglong2 w1 = v2[1];
+          gptr<const u64x2> v2 = (gptr<const u64x2>)(pin[a] + (lin + 4 * h));
+          const u64x2 w0 = v2[0];
+          const u64x2 w1 = v2[1];
           inw[a][0] = w0.x;
           inw[a][1] = w0.y;
           inw[a][2] = w1.x;
@@ -230,10 +274,10 @@ __global__ void __launch_bounds__(256 * QN, 1)
       if constexpr (KEEP && EARLY) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          const uint64_t *cv = conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff;
+          gptr<const uint64_t> cv = sgpr_ptr(conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff);
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            cvw[half][k] = cv[(row << LOGN2) + l + T::TA * k];
+            cvw[half][k] = cv[lo + T::TA * k];
         }
       }
       if (EARLY && jo < NDIG)
@@ -280,7 +324,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
         // q limb: own digit x = a1 b1 (the NTT-form d2 limb) and P (d0, d1),
         // from the four input words at this thread's natural positions 8 th + k
         if constexpr (F) {
-          const double Pd = f64_from_u52(kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
+          const double Pd = f64_from_u52(KEEP ? kp0 : kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             if (h || !EARLY)
@@ -319,8 +363,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
               const uint64_t d0 = mul_mod(A0, B0, mc);
               const uint64_t d1 = add_mod(mul_mod(A0, B1, mc), mul_mod(A1, B0, mc), q);
               const uint64_t c0 = a0[k] >= q ? a0[k] - q : a0[k], c1 = a1[k] >= q ? a1[k] - q : a1[k];
-              a0[k] = add_mod(c0, mul_shoup(d0, kps[2 * t], kps[2 * t + 1], q), q);
-              a1[k] = add_mod(c1, mul_shoup(d1, kps[2 * t], kps[2 * t + 1], q), q);
+              a0[k] = add_mod(c0, mul_shoup(d0, KEEP ? kp0 : kps[2 * t], KEEP ? kp1 : kps[2 * t + 1], q), q);
+              a1[k] = add_mod(c1, mul_shoup(d1, KEEP ? kp0 : kps[2 * t], KEEP ? kp1 : kps[2 * t + 1], q), q);
             }
           }
         }
@@ -336,11 +380,11 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           const unsigned poly = 2 * p + half;
-          const uint64_t *cv = conv + (((size_t)poly * cv_n + t) << logn) + toff;
+          gptr<const uint64_t> cv = sgpr_ptr(conv + (((size_t)poly * cv_n + t) << logn) + toff);
           V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[(row << LOGN2) + l + T::TA * k]);  // conv (lazy)
+            r[k] = A::load_lazy(EARLY ? cvw[half][k] : cv[lo + T::TA * k]);  // conv (lazy)
           wave_sync();
           rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
           // out = f D^-1 - NTTrows(conv D^-1): both factors already folded in
@@ -361,14 +405,14 @@ __global__ void __launch_bounds__(256 * QN, 1)
           // apart).  Lanes 64 B apart store at ~4.2 TB/s against ~5.6 for
           // that shape (copy kernels, scripts/ubench_lanes.hip): keep 1839 -
           // 1853 -> 1798 - 1814 us per chunk, same box.
-          const int e0 = (th & ~63) * 8, ln = th & 63;
-          ulonglong2 *wr = (ulonglong2 *)(lq + (e0 >> LOGN2) * T::RS);
+          const unsigned e0 = (uint32_t)__builtin_amdgcn_readfirstlane((th & ~63) * 8), ln = (unsigned)th & 63;
+          u64x2 *wr = (u64x2 *)(lq + (e0 >> LOGN2) * T::RS);
           wave_sync();  // the row pass's last reads of these words
 #pragma unroll
           for (int i = 0; i < 4; i++)
-            wr[4 * ln + i] = make_ulonglong2(o[2 * i], o[2 * i + 1]);
+            wr[4 * ln + i] = u64x2{o[2 * i], o[2 * i + 1]};
           wave_sync();
-          ulonglong2 *d2 = (ulonglong2 *)(dst + poly * dst_pstride + ((size_t)t << logn) + toff + e0);
+          gptr<u64x2> d2 = (gptr<u64x2>)sgpr_ptr(dst + poly * dst_pstride + ((size_t)t << logn) + toff + e0);
 #pragma unroll
           for (int i = 0; i < 4; i++)  // (non-temporal stores here: 1840 -> 2245 us per chunk)
             d2[64 * i + ln] = wr[64 * i + ln];
@@ -386,10 +430,10 @@ __global__ void __launch_bounds__(256 * QN, 1)
           }
           wave_sync();
           rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
-          uint64_t *o = dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff;
+          gptr<uint64_t> o = sgpr_ptr(dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff);
 #pragma unroll
           for (int k = 0; k < 8; k++)
-            ST_STREAM(ar.canon(r[k]), &o[(row << LOGN2) + l + T::TA * k]);
+            ST_STREAM(ar.canon(r[k]), &o[lo + T::TA * k]);
         }
       }
     }

@@ -22,6 +22,14 @@ for f in files:
         extra += f"  c5 {d['config5']['value']:.0f}"
         if "value_60bit" in d["config5"]:
             extra += f"  c5-60bit {d['config5']['value_60bit']:.0f}"
+    g = d.get("gemv")
+    if g:
+        extra += f"  gemv {g['value']:.0f}"
+        if "alt_primes" in g:
+            extra += f" (60-bit {g['alt_primes']['value']:.0f})"
+    h = d.get("config5", {}).get("hempc_gemv")
+    if h:
+        extra += f"  c5-gemv {h['value']:.0f}"
     print(f"{os.path.basename(f):16s} {d['value']:9.0f} {d['unit']}{extra}  ms/step {d['ms_per_step']:.3f}")
     if "ntt_roundtrip" in d:
         t = d["ntt_roundtrip"]
