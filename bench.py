@@ -448,6 +448,13 @@ def cstr_loop(steps):
             "max_rel_dev_vs_plaintext": rel, "c_caller": cstr_c_caller()}
 
 
+def product_lib_dir():
+    """The directory of the product library the Python legs load (GPQHE_LIB,
+    as hectr_amd.gpqhe.Engine.product): the C callers link it by name."""
+    lib = os.environ.get("GPQHE_LIB")
+    return os.path.dirname(os.path.abspath(lib)) if lib else os.path.join(ROOT, "hectr_amd", "lib")
+
+
 def cstr_c_caller(reps=3):
     """HECTR's own unchanged harness (`test-hectr cstr-hempc`: 40 steps, C
     caller, its pmu timer around the closed loop) on the product library, as a
@@ -457,7 +464,7 @@ def cstr_c_caller(reps=3):
     exe = os.path.join(ROOT, "oracle", "_ref", "test-hectr")
     if not os.path.exists(exe):
         return None
-    env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "hectr_amd", "lib"), GPQHE_SEED="5")
+    env = dict(os.environ, LD_LIBRARY_PATH=product_lib_dir(), GPQHE_SEED="5")
 
     def run(mode):
         ms = []
@@ -493,7 +500,7 @@ def cstr_c_driver(reps=3, steps=100):
     if not os.path.exists(exe):
         return None
     import numpy as np
-    env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "hectr_amd", "lib"), GPQHE_SEED="5")
+    env = dict(os.environ, LD_LIBRARY_PATH=product_lib_dir(), GPQHE_SEED="5")
     dt = np.dtype([("k", "<u4"), ("x", "<f8", 3), ("u", "<f8", 2)])  # tests/hectr.c:812-817
     fix = np.fromfile(os.path.join(ROOT, "tests", "golden", f"cstr-mpc-{steps}.bin"), dtype=dt)
     ms, keygen, dev = [], None, None

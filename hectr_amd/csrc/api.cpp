@@ -259,6 +259,7 @@ struct C1Prov {
   const uint64_t *pk1;
   unsigned lvl;
   bool sub;
+  bool c0 = false;  // the record of an encryption's c0 poly (SpecGemv), not c1
 };
 static std::unordered_map<const uint64_t *, C1Prov> g_prov;
 struct SpecPat {
@@ -285,6 +286,44 @@ struct SpecModupNext {
   bool pending = false;
 };
 static SpecModupNext g_smu_next;
+
+// Speculative gemv (GPQHE_SPEC_GEMV).  Once the step's encryptions have run
+// (spec_flush_early), the last step's gemvs -- the same encryption slots, the
+// same matrices and keys, HECTR's he_gemv of xhat - xr and uhat - ur, src/
+// hempc.c:253-259 -- run at once on this step's ciphertexts: the inner
+// products on the speculated ModUp digits with the differences formed in the
+// kernel, and the ModDown, into SpecGemv::Y.  That device work then overlaps
+// the caller's host work up to its he_gemv calls (the horizon matrices,
+// src/hempc.c:225-240) instead of running between them and the decode.  A
+// he_gemv whose input is the queued difference of exactly those polys, still
+// holding those encryptions (C1Prov records of c0 and c1, dropped by any
+// write), with the same matrix, keys and key generation, queues a copy of its
+// Y instead; anything else takes the normal path.
+struct SgRec {  // a step's gemv, recorded for the next step's speculation
+  SpecPat pat;
+  std::vector<double> M;
+  GemvDiags dg;  // its one launch's diagonals (evk filled)
+  const he_evk_t *rk;
+  uint64_t gen;
+};
+static std::vector<SgRec> g_sg_next;  // this step's gemvs (in g_spec_pats_next order)
+struct SpecGemv {
+  uint64_t *Y = nullptr;  // [np][2][lvl - 1][n]
+  size_t words = 0;
+  unsigned np = 0, lvl = 0;
+  const uint64_t *x[GemvJobs::MAX][4];  // a0, b0, a1, b1 per pattern
+  uint64_t sa[GemvJobs::MAX], sb[GemvJobs::MAX];
+  SgRec rec[GemvJobs::MAX];
+  bool used[GemvJobs::MAX];
+  bool valid = false;
+};
+static SpecGemv g_sg;
+static unsigned g_sg_taken = 0;  // gpqhe_spec_gemv_taken
+
+extern "C" unsigned gpqhe_spec_gemv_taken(void)
+{
+  return g_sg_taken;
+}
 
 static void prov_forget(const void *obj_data, size_t pstride_words)
 {
@@ -439,6 +478,8 @@ static bool drop_dead_encode(const uint64_t *data)
 // coefficients -- so it overlaps the caller's host work up to its next call
 // that needs them (HECTR's horizon matrices in ctr_hempc, src/hempc.c:225-240)
 // instead of starting at that call.  GPQHE_SPEC_EARLY=0: at that call.
+static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<SgRec> &recs);
+
 static void spec_flush_early()
 {
   static const bool on = env_u("GPQHE_SPEC_EARLY", 1) != 0;
@@ -448,7 +489,10 @@ static void spec_flush_early()
   for (const PendEcd &e : g_pecd)
     if (e.dst)
       return;
+  const std::vector<PendEnc> enc = g_penc;
+  const std::vector<SgRec> recs = g_sg_next;  // the last step's gemvs (flush_pending starts a new record)
   flush_pending();
+  spec_gemv_launch(enc, recs);
 }
 
 static void obj_free(void *vo)
@@ -793,6 +837,9 @@ extern "C" void hectx_exit(void)
   g_smu = SpecModup{};
   g_smu_next = SpecModupNext{};
   g_sa = SpecAttach{};
+  g_sg = SpecGemv{};
+  g_sg_next.clear();
+  g_sg_taken = 0;
   g_prov.clear();
   g_spec_pats_next.clear();
   g_spec_pk1_next = nullptr;
@@ -1136,11 +1183,13 @@ static void flush_pending()
     } else {
       g_spec_next_k = 0;
     }
-    if (i0 == 0)
+    if (i0 == 0) {
       g_spec_pats_next.clear();  // a new step: its gemv inputs are recorded afresh
+      g_sg_next.clear();
+    }
     for (unsigned e = 0; e < k; e++) {
       g_prov[enc[i0 + e].c1] = C1Prov{enc[i0 + e].stream, 0, enc[i0 + e].pk1, lvl, false};
-      g_prov.erase(enc[i0 + e].c0);
+      g_prov[enc[i0 + e].c0] = C1Prov{enc[i0 + e].stream, 0, enc[i0 + e].pk1, lvl, false, true};
     }
     // the speculative noise of exactly these streams: only the combine runs,
     // with the queued plaintexts evaluated from their coefficients
@@ -1348,7 +1397,8 @@ static bool spec_launch()
 // limbs (the two-launch form).  The buffers are free: this step's combine and
 // inner products, which read the current speculation, run before in stream
 // order.  (A second stream for this work measured 3x slower)
-static bool spec_attach(bool one, unsigned glvl)
+static bool spec_attach(bool one, unsigned glvl, const std::vector<SpecPat> &pats = g_spec_pats_next,
+                        const uint64_t *pk1 = g_spec_pk1_next)
 {
   static const bool on = env_u("GPQHE_SPEC", 1) != 0 && env_u("GPQHE_SPEC_ATTACH", 1) != 0;
   const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
@@ -1376,15 +1426,14 @@ static bool spec_attach(bool one, unsigned glvl)
   g_spec.lvl = lvl;
   g_spec.valid = true;
   g_smu.valid = false;
-  const std::vector<SpecPat> &pats = g_spec_pats_next;
-  bool ok = !pats.empty() && g_spec_pk1_next && lvl >= 2;
+  bool ok = !pats.empty() && pk1 && lvl >= 2;
   for (const SpecPat &p : pats)
     ok &= p.oa < k && p.ob < k;
   if (ok) {
     const unsigned np = (unsigned)pats.size(), nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
     const size_t dw = (size_t)np * ndig * nm << G.logn;
     if (g_smu.dwords != dw) {
-      pool_free(g_smu.D);
+      pool_free(g_smu.D);  // stream-ordered: its last reader was launched before
       g_smu.D = (uint64_t *)pool_alloc(dw * 8);
       g_smu.dwords = dw;
     }
@@ -1397,12 +1446,13 @@ static bool spec_attach(bool one, unsigned glvl)
     }
     g_smu_next.np = np;
     g_smu_next.d_stride = (size_t)ndig * nm << G.logn;
-    g_smu_next.pk1 = g_spec_pk1_next;
+    g_smu_next.pk1 = pk1;
     g_smu_next.lvl = lvl;
     g_smu_next.pending = true;
-    g_smu.pats = pats;
+    const std::vector<SpecPat> keep = pats;  // (pats may be g_smu.pats itself)
+    g_smu.pats = keep;
     g_smu.base = g_spec.base;
-    g_smu.pk1 = g_spec_pk1_next;
+    g_smu.pk1 = pk1;
     g_smu.lvl = lvl;
   }
   return true;
@@ -1417,6 +1467,73 @@ static bool spec_modup_launch()
   k_modup_ntt_diffs(g_smu.D, g_smu_next.cd, g_smu_next.np, g_smu_next.d_stride, g_smu_next.pk1, g_smu_next.lvl);
   g_smu.valid = true;
   return true;
+}
+
+// The last step's gemvs on this step's encryptions (SpecGemv), right after
+// their combine: one inner-product launch for both (differences formed in the
+// kernel, the speculated ModUp digits), one ModDown with two outputs, and the
+// next step's speculation attached to them as flush_gemvs would (spec_attach,
+// the patterns predicted to repeat).  Only when every recorded gemv ran one
+// launch of diagonals and the ModUp digits speculated for this step are there.
+static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<SgRec> &recs)
+{
+  static const bool on = env_u("GPQHE_SPEC_GEMV", 1) != 0;
+  g_sg.valid = false;
+  const unsigned np = (unsigned)recs.size(), lvl = enc.empty() ? 0 : enc[0].lvl;
+  if (!on || !np || np > GemvJobs::MAX || !g_smu.valid || g_smu.lvl != lvl || g_smu.base != enc[0].stream ||
+      g_smu.pats.size() != np || lvl < 2)
+    return;
+  for (unsigned i = 0; i < np; i++) {
+    const SgRec &r = recs[i];
+    if (r.pat.oa != g_smu.pats[i].oa || r.pat.ob != g_smu.pats[i].ob || r.pat.oa >= enc.size() ||
+        r.pat.ob >= enc.size() || r.gen != g_key_gen || !r.dg.count)
+      return;
+  }
+  const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
+  const size_t n = G.n, dstride = (size_t)ndig * nm * n, ypw = (size_t)(lvl - 1) * n;
+  const size_t words = (size_t)np * 2 * ypw;
+  if (g_sg.words != words) {
+    pool_free(g_sg.Y);  // stream-ordered: its last reader (a queued copy) ran before
+    g_sg.Y = (uint64_t *)pool_alloc(words * 8);
+    g_sg.words = words;
+  }
+  Ws acc((size_t)np * 2 * nm * n);
+  GemvJobs jobs;
+  for (unsigned i = 0; i < np; i++) {
+    const PendEnc &a = enc[recs[i].pat.oa], &b = enc[recs[i].pat.ob];
+    jobs.j[i] = GemvJob{acc.p + (size_t)i * 2 * nm * n, g_smu.D + i * dstride, a.c0, a.c1, recs[i].dg, 0};
+    jobs.j[i].y0 = b.c0;
+    jobs.j[i].y1 = b.c1;
+    g_sg.x[i][0] = a.c0;
+    g_sg.x[i][1] = b.c0;
+    g_sg.x[i][2] = a.c1;
+    g_sg.x[i][3] = b.c1;
+    g_sg.sa[i] = a.stream;
+    g_sg.sb[i] = b.stream;
+    g_sg.rec[i] = recs[i];
+    g_sg.used[i] = false;
+  }
+  // the next step's noise in these launches' idle CUs, its ModUp behind the
+  // decode, for the same patterns (the digits these jobs read are overwritten
+  // only by that ModUp, after the decode in stream order)
+  if (!g_spec_early && spec_attach(true, lvl, std::vector<SpecPat>(g_smu.pats), g_smu.pk1))
+    g_spec_early = true;
+  k_gemv_inner_jobs(jobs, np, lvl);
+  if (np == 1)
+    k_moddown(g_sg.Y, ypw, acc.p, nm * n, 2, lvl, 1);
+  else
+    k_moddown(g_sg.Y, ypw, acc.p, nm * n, 4, lvl, 1, g_sg.Y + 2 * ypw);
+  if (g_sa.sample) {  // (as flush_gemvs: work a launch did not take runs on its own)
+    g_sa.sample = false;
+    k_sample_enc(g_sa.noise, g_sa.stream, g_sa.npoly);
+  }
+  if (g_sa.ntt) {
+    g_sa.ntt = false;
+    k_ntt(g_sa.noise, false);
+  }
+  g_sg.np = np;
+  g_sg.lvl = lvl;
+  g_sg.valid = true;
 }
 
 extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
@@ -1583,8 +1700,8 @@ static void ew_push(uint32_t kind, uint64_t *out, const uint64_t *a, const uint6
   bool known = false;
   if (kind == EW_SUB && !g_prov.empty()) {
     auto ia = g_prov.find(a), ib = g_prov.find(b);
-    if (ia != g_prov.end() && ib != g_prov.end() && !ia->second.sub && !ib->second.sub &&
-        ia->second.pk1 == ib->second.pk1 && ia->second.lvl == lvl && ib->second.lvl == lvl) {
+    if (ia != g_prov.end() && ib != g_prov.end() && !ia->second.sub && !ib->second.sub && !ia->second.c0 &&
+        !ib->second.c0 && ia->second.pk1 == ib->second.pk1 && ia->second.lvl == lvl && ib->second.lvl == lvl) {
       d = C1Prov{ia->second.sa, ib->second.sa, ia->second.pk1, lvl, true};
       known = true;
     }
@@ -1884,6 +2001,87 @@ extern "C" void he_rot(he_ct_t *out, const he_ct_t *in, unsigned int rot, const 
 // Encoded diagonals are cached by content (the caller recomputes the same
 // gain matrices every control step: reference src/hempc.c:232-238).
 // ---------------------------------------------------------------------------
+// A he_gemv of SpecGemv pattern i: y <- Y_i as two queued copies.  Returns
+// i, or -1 (the normal path).
+static int spec_gemv_take(he_ct_t *y, const double *Md, const he_ct_t *x, const he_evk_t rk[])
+{
+  if (!g_sg.valid || x->nlimbs != g_sg.lvl || !g_pgemv.empty() || !defer_ok(0))
+    return -1;
+  const unsigned lvl = g_sg.lvl, s = G.slots;
+  // x = a - b: the last queued op writing each of its polys is a he_sub
+  const uint64_t *lz[4] = {};
+  const uint64_t *xp[2] = {limb(x, 0, 0), limb(x, 1, 0)};
+  for (unsigned j = 0; j < g_pew.count; j++)
+    for (unsigned p = 0; p < 2; p++)
+      if (g_pew.op[j].out == xp[p]) {
+        const EwOp &o = g_pew.op[j];
+        const bool sub = o.kind == EW_SUB && o.lvl >= lvl;
+        lz[2 * p] = sub ? o.a : nullptr;
+        lz[2 * p + 1] = sub ? o.b : nullptr;
+      }
+  if (!lz[0] || !lz[2])
+    return -1;
+  // y must not be an operand of the queued ops (the copies run in the queue's
+  // order, and a later op reading y would read the copy)
+  const uint64_t *ylo = y->data, *yhi = y->data + 2 * pstride(y);
+  auto hits = [&](const uint64_t *q, unsigned l) { return q && q < yhi && q + ((size_t)l << G.logn) > ylo; };
+  for (unsigned j = 0; j < g_pew.count; j++) {
+    const EwOp &o = g_pew.op[j];
+    if (hits(o.a, o.lvl) || hits(o.b, o.lvl) || hits(o.s, o.lvl))
+      return -1;
+  }
+  auto fresh = [&](const uint64_t *p, uint64_t stream, bool c0) {
+    auto it = g_prov.find(p);
+    return it != g_prov.end() && !it->second.sub && it->second.c0 == c0 && it->second.sa == stream &&
+           it->second.lvl == lvl;
+  };
+  for (unsigned i = 0; i < g_sg.np; i++) {
+    const SgRec &r = g_sg.rec[i];
+    if (g_sg.used[i] || lz[0] != g_sg.x[i][0] || lz[1] != g_sg.x[i][1] || lz[2] != g_sg.x[i][2] ||
+        lz[3] != g_sg.x[i][3] || r.rk != rk || r.gen != g_key_gen || r.M.size() != 2 * (size_t)s * s ||
+        memcmp(r.M.data(), Md, r.M.size() * 8) || !fresh(lz[0], g_sg.sa[i], true) ||
+        !fresh(lz[1], g_sg.sb[i], true) || !fresh(lz[2], g_sg.sa[i], false) || !fresh(lz[3], g_sg.sb[i], false))
+      continue;
+    const size_t ypw = (size_t)(lvl - 1) << G.logn;
+    const uint64_t *Y = g_sg.Y + (size_t)i * 2 * ypw;
+    if (!ew_defer(2))
+      return -1;
+    g_sg.used[i] = true;
+    g_sg_taken++;
+    prov_forget(y->data, pstride(y));
+    for (unsigned p = 0; p < 2; p++)
+      ew_push(EW_COPY, limb(y, p, 0), Y + p * ypw, nullptr, nullptr, lvl - 1);
+    return (int)i;
+  }
+  return -1;
+}
+
+// The pattern of a gemv input c whose c1 is the difference of two of this
+// step's encryptions (C1Prov), recorded for the next step's speculation:
+// its index in g_spec_pats_next, or -1.
+static int spec_record_pattern(const C1Prov &c, unsigned lvl)
+{
+  const uint64_t span = 3 * (uint64_t)g_spec_next_k;
+  if (g_spec_next_k && lvl == g_spec_next_lvl && c.sa >= g_step_base && c.sb >= g_step_base &&
+      c.sa < g_step_base + span && c.sb < g_step_base + span && (c.sa - g_step_base) % 3 == 0 &&
+      (c.sb - g_step_base) % 3 == 0 && g_spec_pats_next.size() < XPtrs::MAX &&
+      (g_spec_pats_next.empty() || g_spec_pk1_next == c.pk1)) {
+    g_spec_pk1_next = c.pk1;
+    g_spec_pats_next.push_back({(unsigned)((c.sa - g_step_base) / 3), (unsigned)((c.sb - g_step_base) / 3)});
+    return (int)g_spec_pats_next.size() - 1;
+  }
+  return -1;
+}
+
+// ... and the gemv itself (SgRec), when it is one launch of diagonals
+static void spec_record_gemv(int pat, const double *Md, const PendGemv &pg, const he_evk_t rk[])
+{
+  if (pat < 0 || pg.dgs.size() != 1 || (size_t)pat != g_sg_next.size())
+    return;
+  const size_t mwords = 2 * (size_t)G.slots * G.slots;
+  g_sg_next.push_back({g_spec_pats_next[pat], std::vector<double>(Md, Md + mwords), pg.dgs[0], rk, g_key_gen});
+}
+
 static std::unordered_map<std::string, uint64_t *> g_gemv_cache;
 static std::vector<void *> g_gemv_blocks;  // what the cache's entries live in (one entry or a batch)
 static size_t g_gemv_cache_bytes = 0;
@@ -2133,6 +2331,25 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     gpqhe_die("context not initialised (hectx_init)");
   // x may be a queued difference: left queued when the inner products can
   // form it (ew_lazy_sub, only with x's ModUp digits precomputed), else run
+  // the result speculated at this step's encryptions (SpecGemv): two queued
+  // copies, and the pattern recorded for the next step as below (before
+  // anything flushes the queued differences it matches)
+  if (g_sg.valid && g_pecd.empty() && g_penc.empty()) {
+    if (const int i = spec_gemv_take(y, (const double *)M, x, rk); i >= 0) {
+      const unsigned lvl = x->nlimbs;
+      auto pv = g_prov.find(limb(x, 1, 0));
+      const int pat =
+          pv != g_prov.end() && pv->second.sub && pv->second.lvl == lvl ? spec_record_pattern(pv->second, lvl) : -1;
+      if (pat >= 0 && (size_t)pat == g_sg_next.size()) {
+        const SgRec &r = g_sg.rec[i];
+        g_sg_next.push_back({g_spec_pats_next[pat], r.M, r.dg, rk, g_key_gen});
+      }
+      y->nlimbs = lvl - 1;
+      y->scale = x->scale;
+      y->flags = 0;
+      return;
+    }
+  }
   const uint64_t *lz[4];
   const bool lazy = ew_lazy_sub(y, x, lz);
   if (!lazy)
@@ -2184,6 +2401,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
   }
   PendGemv pg{y->data, pstride(y), limb(x, 0, 0), limb(x, 1, 0), x->data, lvl, {}};
   prov_forget(y->data, pstride(y));
+  int pat = -1;  // the pattern recorded for the next step's speculation
   // x's c1: the difference of two fresh encryptions of this step?  Then its
   // ModUp may be precomputed (SpecModup), and the pattern is kept for the
   // next step's speculation.
@@ -2197,14 +2415,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
           pg.dspec = g_smu.D + i * ((size_t)ndx * nmx << G.logn);
           break;
         }
-    const uint64_t span = 3 * (uint64_t)g_spec_next_k;
-    if (g_spec_next_k && lvl == g_spec_next_lvl && c.sa >= g_step_base && c.sb >= g_step_base &&
-        c.sa < g_step_base + span && c.sb < g_step_base + span && (c.sa - g_step_base) % 3 == 0 &&
-        (c.sb - g_step_base) % 3 == 0 && g_spec_pats_next.size() < XPtrs::MAX &&
-        (g_spec_pats_next.empty() || g_spec_pk1_next == c.pk1)) {
-      g_spec_pk1_next = c.pk1;
-      g_spec_pats_next.push_back({(unsigned)((c.sa - g_step_base) / 3), (unsigned)((c.sb - g_step_base) / 3)});
-    }
+    pat = spec_record_pattern(c, lvl);
   }
   if (lazy && pg.dspec) {
     pg.la0 = lz[0];
@@ -2222,6 +2433,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
       for (GemvDiags &dg : pg.dgs)
         for (unsigned e = 0; e < dg.count; e++, r++)
           dg.evk[e] = gm.rot[r] ? find_rot_key(rk, gm.rot[r], dg.g[e])->data : nullptr;
+      spec_record_gemv(pat, Md, pg, rk);
       g_pgemv.push_back(std::move(pg));
       if (!defer)
         flush_gemvs();
@@ -2309,6 +2521,7 @@ extern "C" void he_gemv(he_ct_t *y, const gpqhe_complex_t M[], const he_ct_t *x,
     g_gemv_mats.erase(g_gemv_mats.begin());
   g_gemv_mats.push_back({s, lvl, std::vector<double>(Md, Md + mwords), pg.dgs, rots});
   const double scale = x->scale;
+  spec_record_gemv(pat, Md, pg, rk);
   g_pgemv.push_back(std::move(pg));
   if (!defer)
     flush_gemvs();

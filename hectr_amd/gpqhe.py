@@ -138,6 +138,7 @@ SIGNATURES = {
     "he_evk_meta": (None, [OBJ, P(C.c_uint32), P(C.c_uint32)]),
     "gpqhe_prof_enable": (None, [C.c_int]),
     "gpqhe_prof_collect": (C.c_uint, [P(KStat), C.c_uint]),
+    "gpqhe_spec_gemv_taken": (C.c_uint, []),
 }
 
 #: symbols declared in include/gpqhe.h (checked by tests/test_abi.py)

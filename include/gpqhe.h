@@ -237,6 +237,9 @@ typedef struct gpqhe_kstat {
 } gpqhe_kstat_t;
 void     gpqhe_prof_enable(int on);
 unsigned gpqhe_prof_collect(gpqhe_kstat_t *out, unsigned max);
+/* [ext] he_gemv calls served by the speculated gemv of the small-N step     */
+/* (api.cpp SpecGemv) since hectx_init; the oracle returns 0.                */
+unsigned gpqhe_spec_gemv_taken(void);
 
 /* ------------------------------------------------------------------------ */
 /* [ext] Serialization (host buffers): residues in the payload layout above, */

@@ -30,6 +30,15 @@ for f in files:
     h = d.get("config5", {}).get("hempc_gemv")
     if h:
         extra += f"  c5-gemv {h['value']:.0f}"
+    c = d.get("cstr")
+    if c:
+        extra += f"  cstr-py {c['steps_per_s']:.0f}/s"
+        cc = c.get("c_caller") or {}
+        if "closed_loop_ms_median" in cc:
+            extra += f"  C-harness {cc['closed_loop_ms_median']:.3f} ms/40"
+            c4 = cc.get("config4_c_driver") or {}
+            if "steps_per_s" in c4:
+                extra += f"  c4-driver {c4['steps_per_s']:.0f}/s"
     print(f"{os.path.basename(f):16s} {d['value']:9.0f} {d['unit']}{extra}  ms/step {d['ms_per_step']:.3f}")
     if "ntt_roundtrip" in d:
         t = d["ntt_roundtrip"]

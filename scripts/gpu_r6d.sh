@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 6: the small-N / rotation / teardown GPU tests on the working tree's
+# library, then a same-box A/B of the bench (every leg but the CPU baseline
+# and the NTT roundtrip) between hectr_amd/lib_ab and the working tree's,
+# alternating ROUNDS times, then a kernel trace of the default bench path
+# that must exit cleanly.      RUN=name bash scripts/gpu_r6d.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${RUN:-r6d}
+mkdir -p $OUT
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 1200 python -u -m pytest ${TESTS:-tests/test_gpu_hectr_caller.py tests/test_gpu_cstr.py tests/test_gpu_parity.py tests/test_gpu_rotations.py tests/test_gpu_teardown.py} \
+    ${KSEL:+-k "$KSEL"} -x -v -m gpu --timeout 600 --timeout-method thread > $OUT/pytest.log 2>&1
+  rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log; tail -4 $OUT/pytest.log; [ $rc -eq 0 ] || exit 1
+fi
+B="python bench.py --steps 10 --warmup 2 --no-cpu --no-ntt ${BENCH_ARGS}"
+for r in $(seq 1 ${ROUNDS:-2}); do
+  GPQHE_LIB=hectr_amd/lib_ab/libgpqhe.so timeout -k 10 400 $B > $OUT/bench_base_$r.log 2>&1 || { echo "base bench failed"; tail -5 $OUT/bench_base_$r.log; exit 1; }
+  timeout -k 10 400 $B > $OUT/bench_new_$r.log 2>&1 || { echo "new bench failed"; tail -5 $OUT/bench_new_$r.log; exit 1; }
+  python scripts/ab_summary.py $OUT/bench_base_$r.log $OUT/bench_new_$r.log | grep -v "^    " || true
+done
+python scripts/ab_summary.py $OUT > $OUT/summary.txt || true
+[ -n "$NO_TRACE" ] && exit 0
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr > $OUT/kt.log 2>&1
+rc=$?; echo "rocprofv3 exit $rc" | tee -a $OUT/kt.log; [ $rc -eq 0 ] || exit 1

@@ -152,8 +152,73 @@ def rekeyed_steps(e, seed=1234, rng_seed=41):
     return res
 
 
+def speculative_gemvs(e, seed=1234, rng_seed=53):
+    """HECTR's step with its own call order (all five encodes, all five
+    encryptions, the plaintexts freed: src/ctr.c:461-480, which starts the
+    early combine and, from the third step on, the speculated gemvs of the
+    last step's pattern, api.cpp SpecGemv), and steps where the speculation
+    must not be taken: a gemv matrix that changed, the subtraction's operands
+    swapped, an encryption overwritten before its he_sub, the gemvs in the
+    other order, the rotation keys regenerated in place, and one gemv only."""
+    e.init(**PARAMS_REF)
+    e.set_seed(seed)
+    rng = np.random.default_rng(rng_seed)
+    s = e.slots
+    M1 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
+    M2 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
+    M3 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
+    plan = ["same", "same", "same", "newM", "same", "swap", "same", "clobber", "same", "order", "same", "regen",
+            "same", "one", "same", "same"]
+    zs = [[rng.uniform(-1, 1, s) + 0j for _ in range(5)] for _ in plan]
+    pk, sk, rk = keys(e, rot=True)
+    res = []
+    for kind, zz in zip(plan, zs):
+        if kind == "regen":
+            e.genrk(rk, sk)
+        pts = []
+        for z in zz:
+            pt = e.pt()
+            e.ecd(pt, z)
+            pts.append(pt)
+        cts = []
+        for pt in pts:
+            ct = e.ct()
+            e.enc_pk(ct, pt, pk)
+            cts.append(ct)
+        for pt in pts:
+            e.free(pt)
+        if kind == "clobber":
+            e.add(cts[1], cts[1], cts[4])
+        xd, ud, ya, yb, du = e.ct(), e.ct(), e.ct(), e.ct(), e.ct()
+        if kind == "swap":
+            e.sub(xd, cts[2], cts[1])
+        else:
+            e.sub(xd, cts[1], cts[2])
+        e.sub(ud, cts[3], cts[4])
+        Ma = M3 if kind == "newM" else M1
+        if kind == "order":
+            e.gemv(yb, M2.ravel(), ud, rk)
+            e.gemv(ya, Ma.ravel(), xd, rk)
+        elif kind == "one":
+            e.gemv(ya, Ma.ravel(), xd, rk)
+            e.copy_ct(yb, ya)
+        else:
+            e.gemv(ya, Ma.ravel(), xd, rk)
+            e.gemv(yb, M2.ravel(), ud, rk)
+        e.add(du, ya, yb)
+        e.neg(du)
+        e.add(du, du, cts[0])
+        res += [e.export(ya), e.export(yb), e.export(du)]
+        for x in (xd, ud, ya, yb):
+            e.free(x)
+        res.append(e.decrypt(du, sk))
+        for x in cts + [du]:
+            e.free(x)
+    return res
+
+
 SEQUENCES = {"speculative_noise": speculative_noise, "queued_differences": queued_differences,
-             "rekeyed_steps": rekeyed_steps}
+             "rekeyed_steps": rekeyed_steps, "speculative_gemvs": speculative_gemvs}
 
 
 def mismatches(a, b):

@@ -640,6 +640,21 @@ def test_gemv_of_queued_differences(oracle, product):
     assert mismatches(queued_differences(oracle), queued_differences(product)) == []
 
 
+def test_speculative_gemvs(oracle, product):
+    """The speculated gemv of the small-N step (api.cpp SpecGemv): HECTR's own
+    call order, taken from the third step on, and the steps where it must not
+    be taken (a changed matrix, swapped operands, an encryption overwritten
+    before its he_sub, the gemvs in the other order, keys regenerated in place,
+    one gemv only) -- bit-exact vs the oracle, and the product served some
+    he_gemv calls from the speculation."""
+    from tests.small_n_steps import mismatches, speculative_gemvs
+    want = speculative_gemvs(oracle)
+    got = speculative_gemvs(product)
+    taken = product.lib.gpqhe_spec_gemv_taken()
+    assert mismatches(want, got) == []
+    assert taken >= 10, taken
+
+
 def test_rekey_between_speculative_steps(oracle, product):
     """The speculative ModUp is keyed on the public key's block (api.cpp
     SpecModup / C1Prov): re-keying between steps -- the key freed and a new
@@ -651,7 +666,8 @@ def test_rekey_between_speculative_steps(oracle, product):
 
 
 @pytest.mark.parametrize("switch", ["GPQHE_SPEC", "GPQHE_SPEC_ATTACH", "GPQHE_SPEC_EARLY", "GPQHE_DEFER",
-                                    "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV", "GPQHE_SPEC_ATTACH_TAKE"])
+                                    "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV", "GPQHE_SPEC_ATTACH_TAKE",
+                                    "GPQHE_SPEC_GEMV"])
 def test_small_n_switch_off_paths(switch):
     """Each small-N switch is read once per process (api.cpp static const), so
     its off path runs in a child process (one at a time, nothing else on the
@@ -667,7 +683,7 @@ def test_small_n_switch_off_paths(switch):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    assert res == {k: [] for k in res} and len(res) == 3, res
+    assert res == {k: [] for k in res} and len(res) == 4, res
 
 
 @pytest.mark.parametrize("name", ["ref", "c1"])
