@@ -439,13 +439,14 @@ def cstr_loop(steps):
     t0 = time.perf_counter()
     x, u = pb.simulate(reg)
     dt = time.perf_counter() - t0
+    taken = eng.lib.gpqhe_spec_gemv_taken()  # he_gemv calls served by the speculated gemvs
     reg.close()
     eng.exit()
     rel = float(max(np.max(np.abs(x - xp) / np.abs(xp)), np.max(np.abs(u - up) / np.abs(up))))
     return {"steps": steps, "horizon": pb.horizon, "slots": pb.slots, "steps_per_s": steps / dt,
             "regulator_ms_median": 1e3 * float(np.median(reg.timings)),
             "regulator_ms_first_step": 1e3 * float(reg.timings[0]), "keygen_s": reg.keygen_s,
-            "max_rel_dev_vs_plaintext": rel, "c_caller": cstr_c_caller()}
+            "max_rel_dev_vs_plaintext": rel, "spec_gemv_taken": taken, "c_caller": cstr_c_caller()}
 
 
 def product_lib_dir():

@@ -32,7 +32,7 @@ for f in files:
         extra += f"  c5-gemv {h['value']:.0f}"
     c = d.get("cstr")
     if c:
-        extra += f"  cstr-py {c['steps_per_s']:.0f}/s"
+        extra += f"  cstr-py {c['steps_per_s']:.0f}/s (spec {c.get('spec_gemv_taken')})"
         cc = c.get("c_caller") or {}
         if "closed_loop_ms_median" in cc:
             extra += f"  C-harness {cc['closed_loop_ms_median']:.3f} ms/40"

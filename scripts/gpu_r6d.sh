@@ -24,3 +24,14 @@ python scripts/ab_summary.py $OUT > $OUT/summary.txt || true
 [ -n "$NO_TRACE" ] && exit 0
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr > $OUT/kt.log 2>&1
 rc=$?; echo "rocprofv3 exit $rc" | tee -a $OUT/kt.log; [ $rc -eq 0 ] || exit 1
+# the C harness with and without the speculated gemvs (same library)
+[ -n "$SPEC_AB" ] || exit 0
+for r in 1 2; do
+  for v in 1 0; do
+    GPQHE_SPEC_GEMV=$v timeout -k 10 200 python -c "
+import sys; sys.path.insert(0, '.'); import bench, json
+print('spec_gemv=$v', json.dumps({k: v for k, v in bench.cstr_c_caller(reps=5).items() if k != 'config4_c_driver'}))
+" >> $OUT/spec_ab.txt 2>&1 || exit 1
+  done
+done
+cat $OUT/spec_ab.txt | cut -c1-200

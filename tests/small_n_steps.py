@@ -171,7 +171,7 @@ def speculative_gemvs(e, seed=1234, rng_seed=53):
             "same", "one", "same", "same"]
     zs = [[rng.uniform(-1, 1, s) + 0j for _ in range(5)] for _ in plan]
     pk, sk, rk = keys(e, rot=True)
-    res = []
+    res, keep = [], []
     for kind, zz in zip(plan, zs):
         if kind == "regen":
             e.genrk(rk, sk)
@@ -208,12 +208,15 @@ def speculative_gemvs(e, seed=1234, rng_seed=53):
         e.add(du, ya, yb)
         e.neg(du)
         e.add(du, du, cts[0])
-        res += [e.export(ya), e.export(yb), e.export(du)]
-        for x in (xd, ud, ya, yb):
+        # (exported after the last step: an export runs every queue and
+        # forgets the speculation records, as any non-queued call does)
+        keep += [ya, yb, du]
+        for x in (xd, ud):
             e.free(x)
         res.append(e.decrypt(du, sk))
-        for x in cts + [du]:
+        for x in cts:
             e.free(x)
+    res += [e.export(x) for x in keep]
     return res
 
 
