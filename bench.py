@@ -439,7 +439,8 @@ def cstr_loop(steps):
     t0 = time.perf_counter()
     x, u = pb.simulate(reg)
     dt = time.perf_counter() - t0
-    taken = eng.lib.gpqhe_spec_gemv_taken()  # he_gemv calls served by the speculated gemvs
+    # he_gemv calls served by the speculated gemvs (absent from older A/B baselines)
+    taken = eng.lib.gpqhe_spec_gemv_taken() if hasattr(eng.lib, "gpqhe_spec_gemv_taken") else None
     reg.close()
     eng.exit()
     rel = float(max(np.max(np.abs(x - xp) / np.abs(xp)), np.max(np.abs(u - up) / np.abs(up))))
