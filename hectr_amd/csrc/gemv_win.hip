@@ -316,6 +316,10 @@ struct GwAcc3 {
 // (and the c0 pass its accumulator words): 8 against before diagonal 0 (the
 // round-5 A/B, profiles/r5_ab_gemv_srcat.json: 4 and 12 within noise of 8)
 constexpr int GW_SRC_AT = 8;
+// the integer forms' counted loop: at the last diagonal (1) or at GW_SRC_AT
+#ifndef GW_INT_SRC_LAST
+#define GW_INT_SRC_LAST 1
+#endif
 // KF (launches of 8 diagonals and more): the FP64 key words are requested on
 // every path of the unrolled diagonal loop (past E at the last diagonal's
 // address); else under each diagonal's branch, where the compiler's wait
@@ -479,10 +483,14 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
         }
       }
     };
-    if constexpr (INT && !KF) {
-      // a launch of a few diagonals (rotations): one diagonal at a time with
-      // the next diagonal's key words in flight (the unrolled form below
-      // spilled 18-64 B/lane for them)
+    if constexpr (INT) {
+      // one diagonal at a time with the next diagonal's key words in flight
+      // (unrolled over 16 like the FP64 forms, the compiler unrolled it only
+      // partly and indexed the key sets through gpr_idx: 60-bit gemv 70.4 ->
+      // 73.3 us, same box, profiles/r6_ab_session1.txt).  The next advance's
+      // source block is requested at the last diagonal: requested earlier, the
+      // wait for the next diagonal's keys at the loop head (vmcnt(0): the
+      // count differs between the iterations) waited it out as well
       uint64_t kc[KW + 1], kn[KW + 1];  // (word KW: the P pt_d word, C0IN q slots)
       auto load_keys1 = [&](int e, uint64_t (&kk)[KW + 1]) {
         const ulonglong2 *kp = (const ulonglong2 *)(Kt + ((((size_t)e) << logn) + koff) * KW);
@@ -501,7 +509,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
           kc[w] = kn[w];
         if (e + 1 < E)
           load_keys1(e + 1, kn);
-        if (e == e_src && more)
+        if (e == (GW_INT_SRC_LAST ? E - 1 : e_src) && more)
           load_src(ob + 16 + dmax + wv);
         int_diag(e, kc, (o + a.d[e]) & (RING - 1), gw_brev((tr[e] + ((a.hm[e] * jh) & 63)) & 63, 6));
       }
@@ -526,7 +534,7 @@ __global__ void __launch_bounds__(1024) gemv_win_kernel(GemvWin a)
     // (KF: key words requested on every path, past E at the last diagonal's:
     // a load under the diagonal's branch left the compiler's wait counts
     // conservative at the joins, a full vmcnt(0) after it)
-    constexpr bool UNR = !INT || KF;  // the unrolled loop below runs this launch
+    constexpr bool UNR = !INT;  // the unrolled loop below runs this launch
 #pragma unroll
     for (int e = 0; e < KD - 1; e++)
       if (UNR && (KF || e < E))
@@ -1009,18 +1017,18 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
             break;
           case 3:
             if (split)
-              !C0 && c.E >= 8 ? go(gemv_win_kernel<1, 16, true, true, false, true>) : go(gemv_win_kernel<1, 16, true, true, C0>);
+              go(gemv_win_kernel<1, 16, true, true, C0>);
             else
-              !C0 && c.E >= 8 ? go(gemv_win_kernel<1, 16, true, false, false, true>) : go(gemv_win_kernel<1, 16, true, false, C0>);
+              go(gemv_win_kernel<1, 16, true, false, C0>);
             break;
           case 4:
             c.E >= 8 ? go(gemv_win_kernel<2, 16, false, false, C0, true>) : go(gemv_win_kernel<2, 16, false, false, C0>);
             break;
           case 5:
             if (split)
-              !C0 && c.E >= 8 ? go(gemv_win_kernel<2, 16, true, true, false, true>) : go(gemv_win_kernel<2, 16, true, true, C0>);
+              go(gemv_win_kernel<2, 16, true, true, C0>);
             else
-              !C0 && c.E >= 8 ? go(gemv_win_kernel<2, 16, true, false, false, true>) : go(gemv_win_kernel<2, 16, true, false, C0>);
+              go(gemv_win_kernel<2, 16, true, false, C0>);
             break;
           default: break;
           }
@@ -1029,9 +1037,9 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
           if (!ic)
             c.E >= 8 ? go(gemv_win_kernel<3, 16, false, false, true, true>) : go(gemv_win_kernel<3, 16, false, false, true>);
           else if (split)
-            c.E >= 8 ? go(gemv_win_kernel<3, 16, true, true, true, true>) : go(gemv_win_kernel<3, 16, true, true, true>);
+            go(gemv_win_kernel<3, 16, true, true, true>);
           else
-            c.E >= 8 ? go(gemv_win_kernel<3, 16, true, false, true, true>) : go(gemv_win_kernel<3, 16, true, false, true>);
+            go(gemv_win_kernel<3, 16, true, false, true>);
         } else if (c0in) {
           form(std::true_type{});
         } else {
