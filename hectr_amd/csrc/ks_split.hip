@@ -37,8 +37,10 @@
 #ifndef KSQ_SPLIT_AR
 #define KSQ_SPLIT_AR 1
 #endif
+// the pair stream as a wave-uniform scalar (sgpr_ptr, below): bit 0 the
+// dropped slots' kernel, bit 1 the kept slots'
 #ifndef KSQ_SCALAR_Q
-#define KSQ_SCALAR_Q 1
+#define KSQ_SCALAR_Q 3
 #endif
 #ifndef KSQ_C5_DROP_LTW
 #define KSQ_C5_DROP_LTW 2
@@ -86,9 +88,11 @@
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 template <class P>
 using gptr = __attribute__((address_space(1))) P *;  // a global-memory pointer
-template <class P>
+template <bool SQ = true, class P>
 __device__ __forceinline__ gptr<P> sgpr_ptr(P *p)
 {
+  if constexpr (!SQ)
+    return (gptr<P>)p;
 #if KSQ_SCALAR_Q
   // (readfirstlane: an opaque scalar; the cast back to the global address
   // space keeps global_load / global_store, not flat, instructions)
@@ -173,11 +177,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
   // the quarter (pair stream) is wave-uniform: as a scalar, the pair index,
   // the loop bound tests and the streams' base addresses live in SGPRs (no
   // exec-masked pair loop, 32-bit lane offsets)
-#if KSQ_SCALAR_Q
-  const int qi = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
-#else
-  const int qi = threadIdx.x >> 8;
-#endif
+  constexpr bool SQ = (KSQ_SCALAR_Q >> (KEEP ? 1 : 0)) & 1;
+  const int qi = SQ ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : (int)(threadIdx.x >> 8);
   const int th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
   // this lane's word offset in a row tile (32-bit, so a uniform base in SGPRs
   // plus it is one global access with a scalar base)
@@ -187,7 +188,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
   const int nx = jo < NDIG ? NDIG - 1 : NDIG;
   auto jof = [&](int u) -> unsigned { return (unsigned)u < jo ? (unsigned)u : (unsigned)u + 1; };
   auto fetch = [&](uint64_t (&x)[8], unsigned j, unsigned p) {
-    gptr<const uint64_t> s = sgpr_ptr(T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff);
+    gptr<const uint64_t> s = sgpr_ptr<SQ>(T1 + p * t1_stride + (((size_t)j * nm + t) << logn) + toff);
 #pragma unroll
     for (int k = 0; k < 8; k++)
       x[k] = s[lo + T::TA * k];
@@ -250,8 +251,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
       // the dropped q slot's first half of input words is requested here, so
       // its latency overlaps the converted limb's row pass (1037 -> 1018 us)
       const size_t ioff = p * d01.in_stride + ((size_t)t << logn) + toff;  // (uniform)
-      gptr<const uint64_t> pin[4] = {sgpr_ptr(d01.a + ioff), sgpr_ptr(d01.b + ioff), sgpr_ptr(d01.a + ioff + d01.in_pstride),
-                                sgpr_ptr(d01.b + ioff + d01.in_pstride)};  // a0, b0, a1, b1
+      gptr<const uint64_t> pin[4] = {sgpr_ptr<SQ>(d01.a + ioff), sgpr_ptr<SQ>(d01.b + ioff), sgpr_ptr<SQ>(d01.a + ioff + d01.in_pstride),
+                                sgpr_ptr<SQ>(d01.b + ioff + d01.in_pstride)};  // a0, b0, a1, b1
       const unsigned lin = 8u * (unsigned)th;
       uint64_t inw[4][4];
       auto ld_in = [&](int h) {
@@ -274,7 +275,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
       if constexpr (KEEP && EARLY) {
 #pragma unroll
         for (int half = 0; half < 2; half++) {
-          gptr<const uint64_t> cv = sgpr_ptr(conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff);
+          gptr<const uint64_t> cv = sgpr_ptr<SQ>(conv + (((size_t)(2 * p + half) * cv_n + t) << logn) + toff);
 #pragma unroll
           for (int k = 0; k < 8; k++)
             cvw[half][k] = cv[lo + T::TA * k];
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
 #pragma unroll
         for (int half = 0; half < 2; half++) {
           const unsigned poly = 2 * p + half;
-          gptr<const uint64_t> cv = sgpr_ptr(conv + (((size_t)poly * cv_n + t) << logn) + toff);
+          gptr<const uint64_t> cv = sgpr_ptr<SQ>(conv + (((size_t)poly * cv_n + t) << logn) + toff);
           V r[8];
 #pragma unroll
           for (int k = 0; k < 8; k++)
@@ -412,7 +413,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           for (int i = 0; i < 4; i++)
             wr[4 * ln + i] = u64x2{o[2 * i], o[2 * i + 1]};
           wave_sync();
-          gptr<u64x2> d2 = (gptr<u64x2>)sgpr_ptr(dst + poly * dst_pstride + ((size_t)t << logn) + toff + e0);
+          gptr<u64x2> d2 = (gptr<u64x2>)sgpr_ptr<SQ>(dst + poly * dst_pstride + ((size_t)t << logn) + toff + e0);
 #pragma unroll
           for (int i = 0; i < 4; i++)  // (non-temporal stores here: 1840 -> 2245 us per chunk)
             d2[64 * i + ln] = wr[64 * i + ln];
@@ -430,7 +431,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
           }
           wave_sync();
           rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
-          gptr<uint64_t> o = sgpr_ptr(dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff);
+          gptr<uint64_t> o = sgpr_ptr<SQ>(dst + (2 * p + half) * dst_pstride + ((size_t)(t - t_lo) << logn) + toff);
 #pragma unroll
           for (int k = 0; k < 8; k++)
             ST_STREAM(ar.canon(r[k]), &o[lo + T::TA * k]);
