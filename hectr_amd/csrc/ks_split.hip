@@ -39,6 +39,9 @@
 #endif
 // the pair stream as a wave-uniform scalar (sgpr_ptr, below): bit 0 the
 // dropped slots' kernel, bit 1 the kept slots'
+#ifndef KSQ_DROP_PF1
+#define KSQ_DROP_PF1 1
+#endif
 #ifndef KSQ_SCALAR_Q
 #define KSQ_SCALAR_Q 3
 #endif
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
   // [P s_t]_t and its Shoup companion, read before any store of the kernel
   // (a uniform load a store may clobber is a vector load, and its wait,
   // vmcnt(0), also waited out every prefetch in flight)
-  const uint64_t kp0 = KEEP ? kps[2 * t] : 0, kp1 = KEEP ? kps[2 * t + 1] : 0;
+  const uint64_t kp0 = kps[2 * t], kp1 = kps[2 * t + 1];
   for (unsigned idx = threadIdx.x; idx < 2 * NDIG * 2048; idx += 256 * QN) {
     const unsigned c = idx >> 11, w = idx & 2047;
     // plain (FP64 moduli) or Montgomery form: either way x s_t stays in its form
@@ -194,10 +197,16 @@ __global__ void __launch_bounds__(256 * QN, 1)
       x[k] = s[lo + T::TA * k];
   };
   unsigned p = pb0 + qi;
-  uint64_t xn[NX > 0 ? NX : 1][8];
+  // PF1 (the dropped slots' two digits): one tile buffer, each converted limb
+  // requested one phase ahead (the next digit of this pair, or the first of
+  // the next pair) instead of every digit of the next pair at once -- 16 VGPRs
+  // fewer
+  constexpr bool PF1 = !KEEP && NX > 1 && KSQ_DROP_PF1;
+  constexpr int NB = PF1 ? 1 : (NX > 0 ? NX : 1);
+  uint64_t xn[NB][8];
   if (p < pb1)
 #pragma unroll
-    for (int u = 0; u < NX; u++)
+    for (int u = 0; u < NB; u++)
       if (u < nx)
         fetch(xn[u], jof(u), p);
   auto mac_i = [&](uint64_t &a, uint64_t v, uint64_t w) {  // Montgomery MAC, lazy [0, 2q)
@@ -289,11 +298,18 @@ __global__ void __launch_bounds__(256 * QN, 1)
           continue;
         const unsigned j = jof(u);
         V r[8];
+        uint64_t (&xb)[8] = xn[PF1 ? 0 : u];
 #pragma unroll
         for (int k = 0; k < 8; k++)
-          r[k] = A::load_lazy(xn[u][k]);  // T1 (ks_cols4, lazy)
-        if (pn < pb1)
-          fetch(xn[u], j, pn);  // next pair's tile, in flight meanwhile
+          r[k] = A::load_lazy(xb[k]);  // T1 (ks_cols4, lazy)
+        if constexpr (PF1) {
+          if (u + 1 < nx)
+            fetch(xb, jof(u + 1), p);  // this pair's next digit
+          else if (pn < pb1)
+            fetch(xb, jof(0), pn);  // the next pair's first
+        } else if (pn < pb1) {
+          fetch(xb, j, pn);  // next pair's tile, in flight meanwhile
+        }
         wave_sync();            // the previous phase has finished with the LDS tile
         rows8_fwd_raw<LOGN2>(r, lq, ar, n1 + row0, th);
         if constexpr (F) {
@@ -325,7 +341,7 @@ __global__ void __launch_bounds__(256 * QN, 1)
         // q limb: own digit x = a1 b1 (the NTT-form d2 limb) and P (d0, d1),
         // from the four input words at this thread's natural positions 8 th + k
         if constexpr (F) {
-          const double Pd = f64_from_u52(KEEP ? kp0 : kps[2 * t]), Pq = Pd * ar.qinv;  // [P s_t]_t
+          const double Pd = f64_from_u52(kp0), Pq = Pd * ar.qinv;  // [P s_t]_t
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             if (h || !EARLY)
@@ -364,8 +380,8 @@ __global__ void __launch_bounds__(256 * QN, 1)
               const uint64_t d0 = mul_mod(A0, B0, mc);
               const uint64_t d1 = add_mod(mul_mod(A0, B1, mc), mul_mod(A1, B0, mc), q);
               const uint64_t c0 = a0[k] >= q ? a0[k] - q : a0[k], c1 = a1[k] >= q ? a1[k] - q : a1[k];
-              a0[k] = add_mod(c0, mul_shoup(d0, KEEP ? kp0 : kps[2 * t], KEEP ? kp1 : kps[2 * t + 1], q), q);
-              a1[k] = add_mod(c1, mul_shoup(d1, KEEP ? kp0 : kps[2 * t], KEEP ? kp1 : kps[2 * t + 1], q), q);
+              a0[k] = add_mod(c0, mul_shoup(d0, kp0, kp1, q), q);
+              a1[k] = add_mod(c1, mul_shoup(d1, kp0, kp1, q), q);
             }
           }
         }
@@ -580,9 +596,9 @@ void ksq_run(unsigned logn2, unsigned ndig, bool allf, bool keep_stage, const ui
              const uint64_t *evkm, uint64_t *dst, size_t dst_pstride, const uint64_t *conv, const uint64_t *ksc,
              const uint64_t *kps, unsigned count, unsigned lvl, unsigned nm, unsigned t_lo, unsigned t_n)
 {
-#ifdef KSQ_DEV  // analysis builds: the bench's instantiations only
-  if (logn2 == 8 && ndig == 2 && allf) {
-    ksq_launch<8, 2, 3, 1, 1>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n, t_n);
+#ifdef KSQ_DEV  // analysis builds: the bench's instantiations only (N=2^16: 128 x 512)
+  if (logn2 == 9 && ndig == 2 && allf) {
+    ksq_launch<9, 2, 3, 1, 1>(keep_stage, T1, d01, evkm, dst, dst_pstride, conv, ksc, kps, count, lvl, nm, t_lo, t_n, t_n);
     return;
   }
   gpqhe_die("KSQ_DEV build");
