@@ -379,6 +379,9 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 // (launch bound: two workgroups per CU, 128 VGPRs; the inverse takes 8-byte
 // twiddle entries (W8) to fit: with 16-byte ones it spilled 16 VGPRs, and at
 // one workgroup per CU it ran slower still)
+#ifndef NTT_ROWS_SQ
+#define NTT_ROWS_SQ 1
+#endif
 template <int LOGN2, bool INV, int QN, bool W8 = false, bool DIN = false>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
                                                              const ModConst *mcs, unsigned members)
@@ -398,23 +401,26 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
   const uint64_t q = mcs[m].q;
   const unsigned row0 = tile * T::R;
   const size_t toff = (size_t)row0 << LOGN2;
-  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  // the poly stream is wave-uniform (scalar: SGPR stream bases, 32-bit lane
+  // offsets, a pair loop without exec masks; as the split key switch's ksq)
+  const int qi = NTT_ROWS_SQ ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : (int)(threadIdx.x >> 8);
+  const int th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
   uint64_t *lq = rt[qi];
   auto fetch = [&](uint64_t (&w)[8], unsigned p) {
-    const uint64_t *x = s.limb(p * per + slot, logn) + toff;
+    const auto x = sgpr_ptr<NTT_ROWS_SQ>(s.limb(p * per + slot, logn) + toff);
     if constexpr (INV && DIN) {
       // the thread's round-C words 8 h + k of its row, 16-byte loads
-      const ulonglong2 *v2 = (const ulonglong2 *)(x + (row << LOGN2) + 8 * l);
+      const auto v2 = (gptr<const u64x2>)(x + (unsigned)((row << LOGN2) + 8 * l));
 #pragma unroll
       for (int i = 0; i < 4; i++) {
-        const ulonglong2 v = v2[i];
+        const u64x2 v = v2[i];
         w[2 * i] = v.x;
         w[2 * i + 1] = v.y;
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 8; k++)
-        w[k] = INV ? x[(th & ~63) * 8 + (th & 63) + 64 * k] : x[(row << LOGN2) + l + T::TA * k];
+        w[k] = INV ? x[(unsigned)((th & ~63) * 8 + (th & 63) + 64 * k)] : x[(unsigned)((row << LOGN2) + l + T::TA * k)];
     }
   };
   with_arith(q, m, logn, tw, [&](const auto &ar0) {
@@ -453,12 +459,13 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
         for (int k = 0; k < 8; k++)
           r[k] = std::decay_t<decltype(ar)>::load(w[k]);
         rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
-        uint64_t *y = o.limb(p * per + slot, logn) + toff;
+        const auto y = sgpr_ptr<NTT_ROWS_SQ>(o.limb(p * per + slot, logn) + toff);
 #pragma unroll
         for (int k = 0; k < 8; k++)
-          y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+          y[(unsigned)((row << LOGN2) + l + T::TA * k)] = ar.canon(r[k]);
       } else {
-        rows8_tile_words<LOGN2, INV>(ar, w, o.limb(p * per + slot, logn) + toff, lq, n1 + row0, th);
+        rows8_tile_words<LOGN2, INV>(ar, w, sgpr_ptr<NTT_ROWS_SQ>(o.limb(p * per + slot, logn) + toff), lq, n1 + row0,
+                                     th);
       }
     }
   });
@@ -2759,7 +2766,9 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y
   const double q = (double)mcs[limb].q, qinv = 1.0 / q;
   const unsigned row0 = tile * T::R;
   const size_t off = ((size_t)limb << logn) + ((size_t)row0 << LOGN2);
-  const int qi = threadIdx.x >> 8, th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
+  // (the pair stream wave-uniform: scalar stream bases, as ntt_rows_q_kernel)
+  const int qi = NTT_ROWS_SQ ? (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 8) : (int)(threadIdx.x >> 8);
+  const int th = threadIdx.x & 255, row = th / T::TA, l = th % T::TA;
   uint64_t *lq = rt[qi];
   const size_t o = (size_t)limb << (logn + 1);
   RowTw<LOGN2>::template stage<true>(rtw, (const uint64_t *)(tw.invd + o), n1 + row0, threadIdx.x, 256 * QN);
@@ -2768,15 +2777,15 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y
   const double sd = f64_from_u52(ysc[2 * limb]);
   // this thread's 8 consecutive words 8 th + k: its round-C elements
   auto fetch = [&](uint64_t (&A1)[8], uint64_t (&B1)[8], unsigned p) {
-    const ulonglong2 *pa = (const ulonglong2 *)(a + p * in_stride + in_pstride + off + 8 * th);
-    const ulonglong2 *pb = (const ulonglong2 *)((ONE ? a : b) + p * in_stride + in_pstride + off + 8 * th);
+    const auto pa = (gptr<const u64x2>)(sgpr_ptr<NTT_ROWS_SQ>(a + p * in_stride + in_pstride + off) + 8u * th);
+    const auto pb = (gptr<const u64x2>)(sgpr_ptr<NTT_ROWS_SQ>((ONE ? a : b) + p * in_stride + in_pstride + off) + 8u * th);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const ulonglong2 x = pa[i];
+      const u64x2 x = pa[i];
       A1[2 * i] = x.x;
       A1[2 * i + 1] = x.y;
       if constexpr (!ONE) {
-        const ulonglong2 z = pb[i];
+        const u64x2 z = pb[i];
         B1[2 * i] = z.x;
         B1[2 * i + 1] = z.y;
       }
@@ -2804,10 +2813,10 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) d2_rows_q_kernel(uint64_t *y
       fetch(nA, nB, p + QN);  // the next pair's words, in flight meanwhile
     wave_sync();              // the previous pair's rounds have finished with the LDS tile
     rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
-    uint64_t *yo = y + (size_t)p * lvl * ((size_t)1 << logn) + off;
+    const auto yo = sgpr_ptr<NTT_ROWS_SQ>(y + (size_t)p * lvl * ((size_t)1 << logn) + off);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      ST_STREAM(ar.canon(r[k]), &yo[(row << LOGN2) + l + T::TA * k]);
+      ST_STREAM(ar.canon(r[k]), &yo[(unsigned)((row << LOGN2) + l + T::TA * k)]);
   }
 }
 

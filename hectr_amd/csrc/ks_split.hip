@@ -84,33 +84,6 @@
 // 2215 us, spills; one kernel per lazy-reduction policy with the slots
 // launched in runs of one policy -- keep 1869, drop 1213 us.  DESIGN 5b.)
 
-// A wave-uniform pointer pinned to SGPRs where it is used: the compiler
-// otherwise hoists (uniform base + lane offset) out of the pair loop as 64-bit
-// VGPR pairs, one per stream, and spills them (each reload's vmcnt(0) then
-// also waits out the prefetches in flight).  The pointer must be uniform.
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-template <class P>
-using gptr = __attribute__((address_space(1))) P *;  // a global-memory pointer
-template <bool SQ = true, class P>
-__device__ __forceinline__ gptr<P> sgpr_ptr(P *p)
-{
-  if constexpr (!SQ)
-    return (gptr<P>)p;
-#if KSQ_SCALAR_Q
-  // (readfirstlane: an opaque scalar; the cast back to the global address
-  // space keeps global_load / global_store, not flat, instructions)
-  // (the builtin returns int: each half goes through uint32_t, or the low
-  // one would be sign-extended into the high one)
-  const uint64_t v = (uint64_t)(uintptr_t)p;
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint64_t s = ((uint64_t)hi << 32) | lo;
-  return (gptr<P>)(P *)(uintptr_t)s;
-#else
-  return (gptr<P>)p;
-#endif
-}
-
 // the policy with its lazy-reduction choice fixed (LZ 0 / 1; -1 as it is)
 template <int LZ>
 __device__ __forceinline__ ArF64 with_lz(ArF64 a)

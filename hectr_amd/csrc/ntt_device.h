@@ -771,6 +771,33 @@ __device__ __forceinline__ void cols_tile(const A &ar, const uint64_t *x, uint64
 // operations of one wave execute in order, the fences only keep the compiler
 // from moving them across the exchange.  Waves of a block never wait for each
 // other.
+// A wave-uniform pointer pinned to SGPRs where it is used (the split key
+// switch's and the NTT row passes' pair / poly streams): the compiler
+// otherwise hoists (uniform base + lane offset) out of the stream loop as
+// 64-bit VGPR pairs, one per stream, and spills them (each reload's vmcnt(0)
+// then also waits out the prefetches in flight).  The pointer must be
+// wave-uniform.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <class P>
+using gptr = __attribute__((address_space(1))) P *;  // a global-memory pointer
+template <bool SQ = true, class P>
+__device__ __forceinline__ gptr<P> sgpr_ptr(P *p)
+{
+  if constexpr (!SQ) {
+    return (gptr<P>)p;
+  } else {
+  // (readfirstlane: an opaque scalar; the cast back to the global address
+  // space keeps global_load / global_store, not flat, instructions)
+  // (the builtin returns int: each half goes through uint32_t, or the low
+  // one would be sign-extended into the high one)
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint64_t s = ((uint64_t)hi << 32) | lo;
+  return (gptr<P>)(P *)(uintptr_t)s;
+  }
+}
+
 __device__ __forceinline__ void wave_sync()
 {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -977,8 +1004,8 @@ __device__ __forceinline__ void rows8_tile_raw(const A &ar, const uint64_t (&raw
 // row-pass input words (row << LOGN2) + l + TA k, lazy; inverse -- the
 // coalesced words wl_elem(i), canonical), output canonical to y in the other
 // layout.  th: the thread's index in its 256-thread tile group.
-template <int LOGN2, bool INV, class A>
-__device__ __forceinline__ void rows8_tile_words(const A &ar, const uint64_t (&w)[8], uint64_t *y, uint64_t *lds,
+template <int LOGN2, bool INV, class A, class Y>
+__device__ __forceinline__ void rows8_tile_words(const A &ar, const uint64_t (&w)[8], Y y, uint64_t *lds,
                                                  uint64_t rowbase0, const int th)
 {
   using T = Row8<LOGN2>;
@@ -998,7 +1025,7 @@ __device__ __forceinline__ void rows8_tile_words(const A &ar, const uint64_t (&w
     wave_sync();
 #pragma unroll
     for (int i = 0; i < 8; i++)
-      y[(th & ~63) * 8 + (th & 63) + 64 * i] = lds[T::wl(th, i)];
+      y[(unsigned)((th & ~63) * 8 + (th & 63) + 64 * i)] = lds[T::wl(th, i)];
   } else {
 #pragma unroll
     for (int i = 0; i < 8; i++)
@@ -1011,7 +1038,7 @@ __device__ __forceinline__ void rows8_tile_words(const A &ar, const uint64_t (&w
     rows8_inv<LOGN2>(r, lds, ar, rowbase0, th);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-      y[(row << LOGN2) + l + T::TA * k] = ar.canon(r[k]);
+      y[(unsigned)((row << LOGN2) + l + T::TA * k)] = ar.canon(r[k]);
   }
 }
 
