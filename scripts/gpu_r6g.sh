@@ -12,7 +12,8 @@ if [ -n "$TESTS" ]; then
     > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest exit $rc" >> $OUT/pytest.log; tail -4 $OUT/pytest.log; [ $rc -eq 0 ] || exit 1
 fi
-B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr ${NTT:+--ntt-polys 1024} ${NTT:---no-ntt} ${BENCH_ARGS}"
+NO_NTT=--no-ntt; [ -n "$NTT" ] && NO_NTT=""
+B="python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr $NO_NTT ${BENCH_ARGS}"
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in ${LIBS:-new=hectr_amd/lib/libgpqhe.so}; do
     GPQHE_LIB=${v#*=} timeout -k 10 400 $B > $OUT/bench_${v%%=*}_$r.log 2>&1 || { echo "bench $v failed"; tail -5 $OUT/bench_${v%%=*}_$r.log; exit 1; }
