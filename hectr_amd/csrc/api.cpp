@@ -308,8 +308,9 @@ struct SgRec {  // a step's gemv, recorded for the next step's speculation
 };
 static std::vector<SgRec> g_sg_next;  // this step's gemvs (in g_spec_pats_next order)
 struct SpecGemv {
-  uint64_t *Y = nullptr;  // [np][2][lvl - 1][n]
-  size_t words = 0;
+  // pattern i's result, in a block shaped as a ciphertext object's (2 polys
+  // of G.L limbs): a taking he_gemv swaps it with its output object's block
+  uint64_t *Y[GemvJobs::MAX] = {};
   unsigned np = 0, lvl = 0;
   const uint64_t *x[GemvJobs::MAX][4];  // a0, b0, a1, b1 per pattern
   uint64_t sa[GemvJobs::MAX], sb[GemvJobs::MAX];
@@ -1490,13 +1491,10 @@ static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<
       return;
   }
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
-  const size_t n = G.n, dstride = (size_t)ndig * nm * n, ypw = (size_t)(lvl - 1) * n;
-  const size_t words = (size_t)np * 2 * ypw;
-  if (g_sg.words != words) {
-    pool_free(g_sg.Y);  // stream-ordered: its last reader (a queued copy) ran before
-    g_sg.Y = (uint64_t *)pool_alloc(words * 8);
-    g_sg.words = words;
-  }
+  const size_t n = G.n, dstride = (size_t)ndig * nm * n, ypw = (size_t)G.L * n;
+  for (unsigned i = 0; i < np; i++)
+    if (!g_sg.Y[i])  // (stream-ordered: a block swapped in last step was last read before this launch)
+      g_sg.Y[i] = (uint64_t *)pool_alloc(2 * ypw * 8);
   Ws acc((size_t)np * 2 * nm * n);
   GemvJobs jobs;
   for (unsigned i = 0; i < np; i++) {
@@ -1520,9 +1518,9 @@ static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<
     g_spec_early = true;
   k_gemv_inner_jobs(jobs, np, lvl);
   if (np == 1)
-    k_moddown(g_sg.Y, ypw, acc.p, nm * n, 2, lvl, 1);
+    k_moddown(g_sg.Y[0], ypw, acc.p, nm * n, 2, lvl, 1);
   else
-    k_moddown(g_sg.Y, ypw, acc.p, nm * n, 4, lvl, 1, g_sg.Y + 2 * ypw);
+    k_moddown(g_sg.Y[0], ypw, acc.p, nm * n, 4, lvl, 1, g_sg.Y[1]);
   if (g_sa.sample) {  // (as flush_gemvs: work a launch did not take runs on its own)
     g_sa.sample = false;
     k_sample_enc(g_sa.noise, g_sa.stream, g_sa.npoly);
@@ -2042,15 +2040,22 @@ static int spec_gemv_take(he_ct_t *y, const double *Md, const he_ct_t *x, const 
         memcmp(r.M.data(), Md, r.M.size() * 8) || !fresh(lz[0], g_sg.sa[i], true) ||
         !fresh(lz[1], g_sg.sb[i], true) || !fresh(lz[2], g_sg.sa[i], false) || !fresh(lz[3], g_sg.sb[i], false))
       continue;
-    const size_t ypw = (size_t)(lvl - 1) << G.logn;
-    const uint64_t *Y = g_sg.Y + (size_t)i * 2 * ypw;
+    const size_t ypw = (size_t)G.L << G.logn;
     if (!ew_defer(2))
       return -1;
     g_sg.used[i] = true;
     g_sg_taken++;
     prov_forget(y->data, pstride(y));
-    for (unsigned p = 0; p < 2; p++)
-      ew_push(EW_COPY, limb(y, p, 0), Y + p * ypw, nullptr, nullptr, lvl - 1);
+    if (y->npoly == 2 && y->cap == G.L && y->data) {
+      // an object of the engine's own ciphertext shape: its block and Y_i's
+      // trade places (no copy; the old block is the next step's Y_i -- no
+      // queued op can name it: a queued op writing y would have to come
+      // after this call, and the next speculation starts with empty queues)
+      std::swap(y->data, g_sg.Y[i]);
+    } else {
+      for (unsigned p = 0; p < 2; p++)
+        ew_push(EW_COPY, limb(y, p, 0), g_sg.Y[i] + p * ypw, nullptr, nullptr, lvl - 1);
+    }
     return (int)i;
   }
   return -1;
