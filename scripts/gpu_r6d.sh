@@ -21,12 +21,13 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   python scripts/ab_summary.py $OUT/bench_base_$r.log $OUT/bench_new_$r.log | grep -v "^    " || true
 done
 python scripts/ab_summary.py $OUT > $OUT/summary.txt || true
-[ -n "$NO_TRACE" ] && exit 0
+if [ -z "$NO_TRACE" ]; then
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu --no-cstr > $OUT/kt.log 2>&1
 rc=$?; echo "rocprofv3 exit $rc" | tee -a $OUT/kt.log; [ $rc -eq 0 ] || exit 1
+fi
 # the C harness with and without the speculated gemvs (same library)
 [ -n "$SPEC_AB" ] || exit 0
-for r in 1 2; do
+for r in $(seq 1 ${SPEC_ROUNDS:-2}); do
   for v in 1 0; do
     GPQHE_SPEC_GEMV=$v timeout -k 10 200 python -c "
 import sys; sys.path.insert(0, '.'); import bench, json
