@@ -270,6 +270,8 @@ static const uint64_t *g_spec_pk1_next = nullptr;
 struct SpecModup {
   uint64_t *D = nullptr;  // [np][ndig][nm][n]
   size_t dwords = 0;
+  uint64_t *Y = nullptr;  // [np][lvl][n] the split ModUp's hand-off (ModupHalves)
+  size_t ywords = 0;
   std::vector<SpecPat> pats;
   uint64_t base = 0;
   const uint64_t *pk1 = nullptr;
@@ -720,6 +722,14 @@ struct HostProfEntry {
 };
 static std::map<std::string, HostProfEntry> g_hp;
 static double g_hp_outside = 0, g_hp_last = -1;
+// GPQHE_HOSTPROF=2 also keeps every outermost call (name, start, end) and
+// prints one steady-state control step's calls relative to the end of the
+// decode before it (the caller's host timeline between two decodes)
+struct HpEvent {
+  const char *name;
+  double t0, t1;
+};
+static std::vector<HpEvent> g_hp_ev;
 static int g_hp_depth = 0;
 static double hp_now()
 {
@@ -755,6 +765,9 @@ struct HpScope {
       HostProfEntry &e = g_hp[name];
       e.us += g_hp_last - t0;
       e.calls++;
+      static const bool ev = env_u("GPQHE_HOSTPROF", 0) >= 2;
+      if (ev && g_hp_ev.size() < 100000)
+        g_hp_ev.push_back(HpEvent{name, t0, g_hp_last});
     }
   }
 };
@@ -771,6 +784,19 @@ static void hp_report()
   for (auto &kv : g_hp)
     fprintf(stderr, "[gpqhe hostprof] %-12s %8lu calls %10.1f us %8.2f us/call\n", kv.first.c_str(), kv.second.calls,
             kv.second.us, kv.second.us / (double)kv.second.calls);
+  // the calls after the (ndcd/2)-th decode up to and including the next one
+  std::vector<size_t> dcd;
+  for (size_t i = 0; i < g_hp_ev.size(); i++)
+    if (!strcmp(g_hp_ev[i].name, "dcd"))
+      dcd.push_back(i);
+  if (dcd.size() >= 4) {
+    const size_t a = dcd[dcd.size() / 2], b = dcd[dcd.size() / 2 + 1];
+    const double t = g_hp_ev[a].t1;
+    fprintf(stderr, "[gpqhe hostprof] one step, us after the decode before it returned: start end name\n");
+    for (size_t i = a + 1; i <= b; i++)
+      fprintf(stderr, "[gpqhe hostprof] %8.1f %8.1f %s\n", g_hp_ev[i].t0 - t, g_hp_ev[i].t1 - t, g_hp_ev[i].name);
+  }
+  g_hp_ev.clear();
   g_hp.clear();
   g_hp_outside = 0;
   g_hp_last = -1;
@@ -1450,6 +1476,27 @@ static bool spec_attach(bool one, unsigned glvl, const std::vector<SpecPat> &pat
     g_smu_next.pk1 = pk1;
     g_smu_next.lvl = lvl;
     g_smu_next.pending = true;
+    // its first half (the differences' inverse transforms) rides on this
+    // step's ModDown (k_moddown: the launch after the noise transforms), so
+    // only the second half runs behind the decode (GPQHE_SPEC_MODUP_SPLIT=0:
+    // the whole ModUp there)
+    static const bool split = env_u("GPQHE_SPEC_MODUP_SPLIT", 1) != 0;
+    if (split) {
+      const size_t yw = (size_t)np * lvl << G.logn;
+      if (g_smu.ywords != yw) {
+        pool_free(g_smu.Y);  // stream-ordered: its last reader was launched before
+        g_smu.Y = (uint64_t *)pool_alloc(yw * 8);
+        g_smu.ywords = yw;
+      }
+      g_sa.mh.cd = g_smu_next.cd;
+      g_sa.mh.pk1 = pk1;
+      g_sa.mh.D = g_smu.D;
+      g_sa.mh.Y = g_smu.Y;
+      g_sa.mh.d_stride = g_smu_next.d_stride;
+      g_sa.mh.np = np;
+      g_sa.mh.lvl = lvl;
+      g_sa.modup_inv = true;
+    }
     const std::vector<SpecPat> keep = pats;  // (pats may be g_smu.pats itself)
     g_smu.pats = keep;
     g_smu.base = g_spec.base;
@@ -1465,7 +1512,12 @@ static bool spec_modup_launch()
   if (!g_smu_next.pending)
     return false;
   g_smu_next.pending = false;
-  k_modup_ntt_diffs(g_smu.D, g_smu_next.cd, g_smu_next.np, g_smu_next.d_stride, g_smu_next.pk1, g_smu_next.lvl);
+  if (g_sa.modup_inv_done) {  // its first half ran in this step's ModDown
+    g_sa.modup_inv_done = false;
+    k_modup_fwd_diffs(g_sa.mh);
+  } else {
+    k_modup_ntt_diffs(g_smu.D, g_smu_next.cd, g_smu_next.np, g_smu_next.d_stride, g_smu_next.pk1, g_smu_next.lvl);
+  }
   g_smu.valid = true;
   return true;
 }

@@ -364,11 +364,29 @@ struct XPtrs {
 // gemv_inner_kernel sample it (sample), of down_inv_small_kernel run its
 // forward transforms (ntt).  Each launcher takes its part and clears the
 // flag; the values equal those of the separate launches.
+// The next step's speculative ModUp in two halves (ModupHalves): the first,
+// per (difference p, input limb i), writes the difference (NTT form) into its
+// digit's own slot of D and Y[p][i] = INTT(x_i) [(Q_j/q_i)^-1] (coefficient
+// form); the second, per (slot t, digit j, p) outside the digit, the
+// conversion sum of Y and the forward transform mod q_t into D.  Together they
+// write what modup_small_kernel<., DIFF> writes, value for value.
+struct ModupHalves {
+  C1Diffs cd{};
+  const uint64_t *pk1 = nullptr;
+  uint64_t *D = nullptr, *Y = nullptr;  // D [np][ndig][nm][n] (stride d_stride), Y [np][lvl][n]
+  size_t d_stride = 0;
+  unsigned np = 0, lvl = 0;
+};
+void k_modup_fwd_diffs(const ModupHalves &mh);  // the second half (n <= 2^12)
 struct SpecAttach {
   bool sample = false, ntt = false;
   LimbSet noise{};      // 3k polys x lvl limbs (per = lvl)
   uint64_t stream = 0;  // poly y draws from ChaCha stream stream + y
   unsigned npoly = 0;   // 3k
+  // the first ModUp half, as extra workgroups of down_fwd_small_kernel (only
+  // in the launch after the one that took ntt: it reads the transformed noise)
+  bool modup_inv = false, modup_inv_done = false;
+  ModupHalves mh{};
 };
 extern SpecAttach g_sa;
 void k_modup_ntt(uint64_t *D, const XPtrs &x1, unsigned count, size_t d_stride, unsigned lvl);

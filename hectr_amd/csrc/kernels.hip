@@ -3167,6 +3167,86 @@ __global__ void __launch_bounds__(512) modup_small_kernel(uint64_t *D, XPtrs x1,
                                lds);
 }
 
+// The speculative ModUp in two halves (ModupHalves; api.cpp spec_attach).
+// First half, workgroup b < np lvl: difference p = b / lvl at input limb
+// ms = b % lvl, formed at load as modup_small_body<., true> forms it; the
+// value goes to its digit's own slot of D (modup_small_body's copy), and the
+// inverse transform times [(Q_j/q_ms)^-1] to Y[p][ms] (the y its inverse
+// callback forms).  Every other workgroup of modup_small_kernel ran this
+// inverse transform again for its own target slot.
+template <int LOGN>
+__device__ __forceinline__ void modup_inv_half_body(const ModupHalves &mh, const UpTable &tab, const Tw2 &tw,
+                                                    const ModConst *mcs, unsigned b, uint64_t *lds)
+{
+  const unsigned p = b / mh.lvl, ms = b % mh.lvl, nm = tab.nm;
+  unsigned j = 0;
+  while (j + 1 < tab.ndig && ms >= tab.dig[j + 1].lo)
+    j++;
+  const UpDigit *dg = tab.dig + j;
+  const uint64_t yw = dg->y[ms - dg->lo], ywp = dg->yp[ms - dg->lo];
+  const ModConst mc = mcs[ms];
+  const size_t w = (size_t)mh.lvl << LOGN, o = (size_t)ms << LOGN;
+  const uint64_t *va = mh.cd.va[p] + o, *vb = mh.cd.vb[p] + o, *pk = mh.pk1 + o;
+  uint64_t *own = mh.D + p * mh.d_stride + (((size_t)j * nm + ms) << LOGN);
+  uint64_t *y = mh.Y + (size_t)p * w + o;
+  with_arith(mc.q, ms, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_inv<LOGN>(
+        ar, lds,
+        [&](int, int e) {
+          const uint64_t ca = add_mod(va[2 * w + e], mul_mod(va[e], pk[e], mc), mc.q);
+          const uint64_t cb = add_mod(vb[2 * w + e], mul_mod(vb[e], pk[e], mc), mc.q);
+          const uint64_t x = sub_mod(ca, cb, mc.q);
+          own[e] = x;
+          return A::load(x);
+        },
+        [&](int, int e, typename A::V a) { y[e] = mul_shoup(ar.mulc(a, mc.ninv, mc.ninvp), yw, ywp, mc.q); });
+  });
+}
+
+// Second half, grid (nm, ndig, np): slot t outside digit j, the conversion sum
+// of Y in 128 bits, one REDC, the forward transform mod q_t (modup_small_body's
+// tail, same order of terms).
+template <int LOGN>
+__global__ void __launch_bounds__(512) modup_fwd_half_kernel(ModupHalves mh, unsigned L, Tw2 tw, UpTable tab,
+                                                              const ModConst *mcs)
+{
+  constexpr int n = 1 << LOGN;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned t = blockIdx.x, j = blockIdx.y, p = blockIdx.z, nm = tab.nm;
+  const UpDigit *dg = tab.dig + j;
+  const unsigned lo = dg->lo, na = dg->na;
+  if (t >= lo && t < lo + na)
+    return;  // the first half wrote the digit's own slots
+  const int th = threadIdx.x;
+  const uint64_t *cj = tab.c + (size_t)j * 8 * nm;
+  const uint64_t *y = mh.Y + ((size_t)p * mh.lvl << LOGN);
+  unsigned __int128 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    acc[k] = 0;
+  for (unsigned i = 0; i < na; i++) {
+    const uint64_t cw = cj[i * nm + t];
+    const uint64_t *yi = y + ((size_t)(lo + i) << LOGN);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      acc[k] += (unsigned __int128)yi[th + k * (n / 8)] * cw;
+  }
+  const unsigned mt = basis_mod(t, mh.lvl, L);
+  const ModConst mc = mcs[mt];
+  uint64_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    r[k] = redc128((uint64_t)(acc[k] >> 64), (uint64_t)acc[k], mc);
+  uint64_t *out = mh.D + p * mh.d_stride + (((size_t)j * nm + t) << LOGN);
+  with_arith(mc.q, mt, LOGN, tw, [&](const auto &ar) {
+    using A = std::decay_t<decltype(ar)>;
+    small_fwd<LOGN>(
+        ar, lds, [&](int k, int) { return A::load(r[k]); },
+        [&](int, int e, typename A::V a) { out[e] = ar.canon(a); });
+  });
+}
+
 SpecAttach g_sa;
 struct SpecNtt {  // down_inv_small_kernel's attached forward transforms
   LimbSet s;
@@ -3265,14 +3345,23 @@ __global__ void __launch_bounds__(512) down_inv_small_kernel(uint64_t *Y, const 
 // down_fwd_small_kernel, grid (keep, npoly): conversion sum of Y to slot t,
 // forward transform mod q_t, out = (X[t] - conv) [D^-1]_t, as the fused
 // kernel (thread th holds elements th + k n/8 before a forward transform).
+// (Rows y >= npoly of the grid: the next step's first ModUp half,
+// modup_inv_half_body, workgroup (y - npoly) keep + x < mh.np mh.lvl.)
 template <int LOGN>
 __global__ void __launch_bounds__(512) down_fwd_small_kernel(uint64_t *out, uint64_t *out2, unsigned half,
                                                               size_t out_pstride, const uint64_t *Y,
                                                               const uint64_t *X, size_t x_pstride, unsigned lvl,
-                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs)
+                                                              unsigned L, Tw2 tw, DownTable tab, const ModConst *mcs,
+                                                              unsigned npoly, ModupHalves mh, UpTable utab)
 {
   constexpr int n = 1 << LOGN;
   __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  if (blockIdx.y >= npoly) {
+    const unsigned b = (blockIdx.y - npoly) * gridDim.x + blockIdx.x;
+    if (b < mh.np * mh.lvl)
+      modup_inv_half_body<LOGN>(mh, utab, tw, mcs, b, lds);
+    return;
+  }
   const unsigned t = blockIdx.x, p = blockIdx.y;
   const int th = threadIdx.x;
   // X's words of this thread's outputs (the forward transform's last round
@@ -3385,6 +3474,25 @@ void k_modup_ntt_diffs(uint64_t *D, const C1Diffs &cd, unsigned np, size_t d_str
   HIP_CHECK(hipGetLastError());
 }
 
+void k_modup_fwd_diffs(const ModupHalves &mh)
+{
+  UpTable &tab = up_table(mh.lvl);
+  if (G.logn < 10 || G.logn > 12 || !mh.np || mh.np > GPQHE_MAXGRP)
+    gpqhe_die("k_modup_fwd_diffs: %u inputs at n = %u", mh.np, G.n);
+  ProfScope ps(KC_MODUP_SMALL, 8.0 * G.n * mh.np * ((double)mh.lvl + (double)tab.ndig * tab.nm));
+  const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tab.nm, tab.ndig, mh.np), dim3(G.n / 8), 0, G.stream, mh, G.L, tw, tab, G.dev.mc);
+  };
+  if (G.logn == 12)
+    go(modup_fwd_half_kernel<12>);
+  else if (G.logn == 11)
+    go(modup_fwd_half_kernel<11>);
+  else
+    go(modup_fwd_half_kernel<10>);
+  HIP_CHECK(hipGetLastError());
+}
+
 // X: npoly polynomials over basis_qp(lvl) (NTT domain, nm limbs each, stride
 // x_pstride); their drop limbs are overwritten (INTT in place).  With out2,
 // the first npoly/2 results go to out and the rest to out2 (two ciphertexts
@@ -3409,11 +3517,23 @@ void k_moddown(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride,
         xn = g_sa.noise.count;
         g_sa.ntt = false;
       }
+      // the next step's first ModUp half reads the noise transformed by the
+      // inverse launch: only with it
+      ModupHalves mh{};
+      UpTable ut{};
+      unsigned ry = 0;
+      if (xn && g_sa.modup_inv) {
+        mh = g_sa.mh;
+        ut = up_table(mh.lvl);
+        ry = (mh.np * mh.lvl + tab.keep - 1) / tab.keep;
+        g_sa.modup_inv = false;
+        g_sa.modup_inv_done = true;
+      }
       auto go2 = [&](auto kinv, auto kfwd) {
         hipLaunchKernelGGL(kinv, dim3(tab.nd * npoly + xn), dim3(G.n / 8), 0, G.stream, Y, X, x_pstride, lvl, G.L, tw,
                            tab, G.dev.mc, npoly, sn);
-        hipLaunchKernelGGL(kfwd, dim3(tab.keep, npoly), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride, Y, X,
-                           x_pstride, lvl, G.L, tw, tab, G.dev.mc);
+        hipLaunchKernelGGL(kfwd, dim3(tab.keep, npoly + ry), dim3(G.n / 8), 0, G.stream, out, out2, half, out_pstride,
+                           Y, X, x_pstride, lvl, G.L, tw, tab, G.dev.mc, npoly, mh, ut);
       };
       if (G.logn == 12)
         go2(down_inv_small_kernel<12>, down_fwd_small_kernel<12>);
