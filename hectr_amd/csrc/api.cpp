@@ -286,20 +286,8 @@ struct SpecModupNext {
   size_t d_stride = 0;
   const uint64_t *pk1 = nullptr;
   bool pending = false;
-  // the split ModUp's second half, deferred from behind the decode into the
-  // next step's combine (k_enc_combine_m); smu_half2_flush launches it alone
-  // before anything else reads g_smu.D
-  bool half2 = false;
-  ModupHalves mh2{};
 };
 static SpecModupNext g_smu_next;
-static void smu_half2_flush()
-{
-  if (!g_smu_next.half2)
-    return;
-  g_smu_next.half2 = false;
-  k_modup_fwd_diffs(g_smu_next.mh2);
-}
 
 // Speculative gemv (GPQHE_SPEC_GEMV).  Once the step's encryptions have run
 // (spec_flush_early), the last step's gemvs -- the same encryption slots, the
@@ -398,7 +386,6 @@ static void check_ctx()
   g_prov.clear();
   g_smu.valid = false;
   g_smu_next.pending = false;
-  g_smu_next.half2 = false;  // (its digits are invalid now)
   flush_ew();
   if (!g_pgemv.empty())
     flush_gemvs();
@@ -1259,9 +1246,7 @@ static void flush_pending()
         }
         em.row_of[e] = (int32_t)r++;
       }
-      const bool h2 = g_smu_next.half2;
-      g_smu_next.half2 = false;
-      k_enc_combine_m(b, em, k, g_spec.buf + off * 3 * w, enc[i0].pk0, enc[i0].pk1, lvl, h2 ? &g_smu_next.mh2 : nullptr);
+      k_enc_combine_m(b, em, k, g_spec.buf + off * 3 * w, enc[i0].pk0, enc[i0].pk1, lvl);
       i0 = i1;
       continue;
     }
@@ -1376,7 +1361,6 @@ static void *zpin(size_t bytes)
 // of encryptions.  True if launched (the caller then waits on g_dcd_ev).
 static bool spec_launch()
 {
-  g_smu_next.half2 = false;  // superseded: this ModUp writes every digit
   static const bool on = env_u("GPQHE_SPEC", 1) != 0;
   const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
   g_smu_next.pending = false;  // superseded
@@ -1447,7 +1431,6 @@ static bool spec_attach(bool one, unsigned glvl, const std::vector<SpecPat> &pat
   const unsigned k = g_spec_next_k, lvl = g_spec_next_lvl;
   if (!on || !one || !k || !lvl || k > GPQHE_MAXGRP || !defer_ok(0) || G.logn < 10 || G.logn > 12 || G.K < 1)
     return false;
-  smu_half2_flush();  // (its Y and D may be reallocated and rewritten below)
   if ((size_t)3 * k * (G.n / 512) > (size_t)(G.n / 64) * (glvl + G.K))
     return false;
   const size_t w = (size_t)lvl << G.logn, words = 3 * (size_t)k * w;
@@ -1531,13 +1514,7 @@ static bool spec_modup_launch()
   g_smu_next.pending = false;
   if (g_sa.modup_inv_done) {  // its first half ran in this step's ModDown
     g_sa.modup_inv_done = false;
-    static const bool defer = env_u("GPQHE_SPEC_MODUP_DEFER", 1) != 0;
-    if (defer) {  // the second half rides on the next step's combine
-      g_smu_next.mh2 = g_sa.mh;
-      g_smu_next.half2 = true;
-    } else {
-      k_modup_fwd_diffs(g_sa.mh);
-    }
+    k_modup_fwd_diffs(g_sa.mh);
   } else {
     k_modup_ntt_diffs(g_smu.D, g_smu_next.cd, g_smu_next.np, g_smu_next.d_stride, g_smu_next.pk1, g_smu_next.lvl);
   }
@@ -1555,7 +1532,6 @@ static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<
 {
   static const bool on = env_u("GPQHE_SPEC_GEMV", 1) != 0;
   g_sg.valid = false;
-  smu_half2_flush();  // (the digits its inner products read)
   const unsigned np = (unsigned)recs.size(), lvl = enc.empty() ? 0 : enc[0].lvl;
   if (!on || !np || np > GemvJobs::MAX || !g_smu.valid || g_smu.lvl != lvl || g_smu.base != enc[0].stream ||
       g_smu.pats.size() != np || lvl < 2)
@@ -2285,7 +2261,6 @@ static void flush_gemvs()
   const unsigned k = (unsigned)q.size(), lvl = q[0].lvl;
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;
-  smu_half2_flush();  // (precomputed digits are read below)
   // ModUp of the inputs without precomputed digits (SpecModup), in one pass
   const size_t dstride = (size_t)ndig * nm * n;
   unsigned miss = 0;

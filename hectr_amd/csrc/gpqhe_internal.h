@@ -337,7 +337,8 @@ struct EncM {
   int32_t row_of[GPQHE_MAXGRP];
   uint32_t row, clog;
 };
-
+void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
+                     const uint64_t *pk1, unsigned lvl);
 // The c1 of the difference of two fresh encryptions without their plaintexts:
 // c1(a_i) - c1(b_i), c1(x) = v pk1 + e1 of the sampled noise (v, e0, e1) at
 // va[i] / vb[i] (NTT form, lvl limbs each).  k_modup_ntt_diffs: their ModUp,
@@ -377,10 +378,6 @@ struct ModupHalves {
   unsigned np = 0, lvl = 0;
 };
 void k_modup_fwd_diffs(const ModupHalves &mh);  // the second half (n <= 2^12)
-// the combine of enc_batch_m_kernel; mh2: the next step's second ModUp half
-// rides along as extra workgroups
-void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
-                     const uint64_t *pk1, unsigned lvl, const ModupHalves *mh2 = nullptr);
 struct SpecAttach {
   bool sample = false, ntt = false;
   LimbSet noise{};      // 3k polys x lvl limbs (per = lvl)

@@ -1629,29 +1629,10 @@ void k_enc_combine_batch(const EncBatch &b, unsigned k, const uint64_t *vee, con
 // by-value argument, and the lane picks its own.  Lane 0 of the four writes
 // c0, lane 1 c1.  Every value is canonical, so the residues equal those of
 // NTT(m) added by enc_batch_kernel.
-// (LOGN2 > 0: blocks of n / 8 threads, and grid z slices >= k run the next
-// step's second ModUp half, modup_fwd_half_body, block (y gridDim.x + x) of
-// the extra slices = (t, j, p) in that order; api.cpp smu_half2)
-template <int LOGN>
-__device__ void modup_fwd_half_body(const ModupHalves &mh, unsigned L, const Tw2 &tw, const UpTable &tab,
-                                    const ModConst *mcs, unsigned t, unsigned j, unsigned p, uint64_t *lds);
-template <int LOGN2>
-__global__ void __launch_bounds__(512) enc_batch_m_kernel(EncBatch bt, EncM em, const uint64_t *vee,
-                                                           const uint64_t *pk0, const uint64_t *pk1, unsigned logn,
-                                                           unsigned lvl, const ModConst *mc, const uint64_t *tw,
-                                                           unsigned k, ModupHalves mhx, Tw2 tw2, UpTable utab,
-                                                           unsigned L)
+__global__ void enc_batch_m_kernel(EncBatch bt, EncM em, const uint64_t *vee, const uint64_t *pk0,
+                                   const uint64_t *pk1, unsigned logn, unsigned lvl, const ModConst *mc,
+                                   const uint64_t *tw)
 {
-  if constexpr (LOGN2 > 0) {
-    if (blockIdx.z >= k) {
-      __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN2];
-      const unsigned b = ((blockIdx.z - k) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, nm = utab.nm,
-                     nd = utab.ndig;
-      if (b < nm * nd * mhx.np)
-        modup_fwd_half_body<LOGN2>(mhx, L, tw2, utab, mc, b % nm, (b / nm) % nd, b / (nm * nd), lds);
-      return;
-    }
-  }
   const unsigned n = 1u << logn;
   const unsigned g = blockIdx.x * blockDim.x + threadIdx.x, i = g >> 2, b = g & 3;
   if (i >= n)
@@ -1687,33 +1668,13 @@ __global__ void __launch_bounds__(512) enc_batch_m_kernel(EncBatch bt, EncM em, 
     bt.c1[e][o] = add_mod(v[2 * w + o], mul_mod(v[o], pk1[o], m), m.q);
 }
 
-static UpTable &up_table(unsigned lvl);
 void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,
-                     const uint64_t *pk1, unsigned lvl, const ModupHalves *mh2)
+                     const uint64_t *pk1, unsigned lvl)
 {
   if (G.logn > 12 || em.row < 4 || em.row > EncM::MAXROW || (em.row & (em.row - 1)))
     gpqhe_die("k_enc_combine_m: %u values per row at n = %u", em.row, G.n);
-  if (mh2 && G.logn >= 10) {
-    // the next step's second ModUp half in extra z slices (blocks of n / 8)
-    const UpTable &ut = up_table(mh2->lvl);
-    const unsigned bt = G.n / 8, gx = 4 * G.n / bt, per = gx * lvl, nb = ut.nm * ut.ndig * mh2->np;
-    if (!mh2->np || mh2->np > GPQHE_MAXGRP)
-      gpqhe_die("k_enc_combine_m: %u ModUp inputs", mh2->np);
-    const Tw2 tw2{G.tw2, G.itw2, G.twd, G.itwd};
-    auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(gx, lvl, k + (nb + per - 1) / per), dim3(bt), 0, G.stream, b, em, vee, pk0, pk1,
-                         G.logn, lvl, G.dev.mc, G.dev.tw, k, *mh2, tw2, ut, G.L);
-    };
-    if (G.logn == 12)
-      go(enc_batch_m_kernel<12>);
-    else if (G.logn == 11)
-      go(enc_batch_m_kernel<11>);
-    else
-      go(enc_batch_m_kernel<10>);
-  } else {
-    hipLaunchKernelGGL(enc_batch_m_kernel<0>, dim3((4 * G.n + TPB - 1) / TPB, lvl, k), dim3(TPB), 0, G.stream, b, em,
-                       vee, pk0, pk1, G.logn, lvl, G.dev.mc, G.dev.tw, k, ModupHalves{}, Tw2{}, UpTable{}, G.L);
-  }
+  hipLaunchKernelGGL(enc_batch_m_kernel, dim3((4 * G.n + TPB - 1) / TPB, lvl, k), dim3(TPB), 0, G.stream, b, em, vee,
+                     pk0, pk1, G.logn, lvl, G.dev.mc, G.dev.tw);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -3243,18 +3204,16 @@ __device__ __forceinline__ void modup_inv_half_body(const ModupHalves &mh, const
   });
 }
 
-// Second half, per (slot t, digit j, difference p): slot t outside digit j,
-// the conversion sum of Y in 128 bits, one REDC, the forward transform mod q_t
-// (modup_small_body's tail, same order of terms).  Its own launch
-// (modup_fwd_half_kernel, grid (nm, ndig, np)) or extra workgroups of the next
-// step's combine (enc_batch_m_kernel<LOGN>).
+// Second half, grid (nm, ndig, np): slot t outside digit j, the conversion sum
+// of Y in 128 bits, one REDC, the forward transform mod q_t (modup_small_body's
+// tail, same order of terms).
 template <int LOGN>
-__device__ __forceinline__ void modup_fwd_half_body(const ModupHalves &mh, unsigned L, const Tw2 &tw,
-                                                    const UpTable &tab, const ModConst *mcs, unsigned t, unsigned j,
-                                                    unsigned p, uint64_t *lds)
+__global__ void __launch_bounds__(512) modup_fwd_half_kernel(ModupHalves mh, unsigned L, Tw2 tw, UpTable tab,
+                                                              const ModConst *mcs)
 {
   constexpr int n = 1 << LOGN;
-  const unsigned nm = tab.nm;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[n];
+  const unsigned t = blockIdx.x, j = blockIdx.y, p = blockIdx.z, nm = tab.nm;
   const UpDigit *dg = tab.dig + j;
   const unsigned lo = dg->lo, na = dg->na;
   if (t >= lo && t < lo + na)
@@ -3286,14 +3245,6 @@ __device__ __forceinline__ void modup_fwd_half_body(const ModupHalves &mh, unsig
         ar, lds, [&](int k, int) { return A::load(r[k]); },
         [&](int, int e, typename A::V a) { out[e] = ar.canon(a); });
   });
-}
-
-template <int LOGN>
-__global__ void __launch_bounds__(512) modup_fwd_half_kernel(ModupHalves mh, unsigned L, Tw2 tw, UpTable tab,
-                                                              const ModConst *mcs)
-{
-  __shared__ __attribute__((aligned(16))) uint64_t lds[1 << LOGN];
-  modup_fwd_half_body<LOGN>(mh, L, tw, tab, mcs, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
 SpecAttach g_sa;
