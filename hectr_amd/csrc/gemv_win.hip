@@ -1084,6 +1084,7 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     HIP_CHECK(hipMemsetAsync(acc, 0, (size_t)cnt * as * 8, G.stream));
   const unsigned keep = mode == 1 ? lvl - 1 : lvl, nd = nm - keep;
   const bool fused = k_ks_fused_ok() && nd <= 5;
+  bool pre = false;
   if (fused) {
     LimbSet dr{};
     dr.base = acc + ((size_t)keep << logn);
@@ -1092,11 +1093,15 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     dr.stride = (size_t)nm * n;
     for (unsigned d = 0; d < nd; d++)
       dr.mods[d] = (uint8_t)(keep + d < lvl ? keep + d : G.L + (keep + d - lvl));
-    k_ntt_rows(dr, dr, true);
+    // the ModDown scale on the row pass's output, so dn_cols runs its
+    // pre-scaled (staged-constant) form
+    pre = k_ntt_rows_down(dr, lvl, mode);
+    if (!pre)
+      k_ntt_rows(dr, dr, true);
   }
   auto down = [&](uint64_t *o, uint64_t *X, unsigned npoly) {
     if (fused)
-      k_moddown_fused(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode);
+      k_moddown_fused(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode, pre);
     else
       k_moddown(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode);
   };

@@ -459,8 +459,11 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
 // ModDown (mode 0: / P, 1: / P q_{lvl-1}) of X whose drop limbs hold the
 // inverse row pass of their NTT form (k_mul_keyswitch_fused with drop_lo =
 // keep).
+// pre: the drop limbs' row pass also applied n^-1 [(D/d)^-1]_d
+// (k_ntt_rows_down), so the pre-scaled column kernels run.
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode);
+                     unsigned lvl, int mode, bool pre = false);
+bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode);
 bool k_prof_on();
 void k_prof_release();
 // Live kernel statistics (gpqhe_prof_enable): HIP events around one launch

@@ -382,9 +382,14 @@ __global__ void __launch_bounds__(256) ntt3_rows_kernel(LimbSet s, LimbSet o, un
 #ifndef NTT_ROWS_SQ
 #define NTT_ROWS_SQ 1
 #endif
-template <int LOGN2, bool INV, int QN, bool W8 = false, bool DIN = false>
+// POST (inverse, DIN): every output word times the slot's constant post[2 slot]
+// (Shoup companion post[2 slot + 1]), canonical -- the ModDown's n^-1
+// [(D/d)^-1]_d on the dropped limbs before dn_cols' pre-scaled form
+// (k_ntt_rows_down).
+template <int LOGN2, bool INV, int QN, bool W8 = false, bool DIN = false, bool POST = false>
 __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s, LimbSet o, unsigned logn, Tw2 tw,
-                                                             const ModConst *mcs, unsigned members)
+                                                             const ModConst *mcs, unsigned members,
+                                                             const uint64_t *post)
 {
   using T = Row8<LOGN2>;
   __shared__ __attribute__((aligned(16))) uint64_t rt[QN][T::WORDS];
@@ -440,6 +445,19 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
       else
         return row_policy<LOGN2, false>(ar0, rtw, (int64_t)T::R - (int64_t)(n1 + row0));
     }();
+    // POST: the slot's scale (FP64: as double with its quotient factor)
+    uint64_t pw = 0, pwp = 0;
+    double pqd = 0, pqi = 0, pwd = 0, pwq = 0;
+    if constexpr (POST) {
+      pw = post[2 * slot];
+      pwp = post[2 * slot + 1];
+      if constexpr (F) {
+        pqd = (double)q;
+        pqi = 1.0 / pqd;
+        pwd = f64_from_u52(pw);
+        pwq = pwd * pqi;
+      }
+    }
     unsigned p = pb0 + qi;
     uint64_t nx[8];
     if (p < pb1)
@@ -461,8 +479,16 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
         rows8_inv<LOGN2>(r, lq, ar, n1 + row0, th);
         const auto y = sgpr_ptr<NTT_ROWS_SQ>(o.limb(p * per + slot, logn) + toff);
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-          y[(unsigned)((row << LOGN2) + l + T::TA * k)] = ar.canon(r[k]);
+        for (int k = 0; k < 8; k++) {
+          if constexpr (POST && F) {  // (constants hoisted out of the poly loop)
+            y[(unsigned)((row << LOGN2) + l + T::TA * k)] =
+                f64_canon(f64_mulmod(f64_from_u52(ar.canon(r[k])), pwd, pwq, pqd), pqd, pqi);
+          } else if constexpr (POST) {
+            y[(unsigned)((row << LOGN2) + l + T::TA * k)] = mul_shoup(ar.canon(r[k]), pw, pwp, q);
+          } else {
+            y[(unsigned)((row << LOGN2) + l + T::TA * k)] = ar.canon(r[k]);
+          }
+        }
       } else {
         rows8_tile_words<LOGN2, INV>(ar, w, sgpr_ptr<NTT_ROWS_SQ>(o.limb(p * per + slot, logn) + toff), lq, n1 + row0,
                                      th);
@@ -475,7 +501,7 @@ __global__ void __launch_bounds__(256 * QN, 2 * QN) ntt_rows_q_kernel(LimbSet s,
 // batched form when every slot has polys enough to share a workgroup's
 // staged twiddles, else one tile per workgroup.
 template <int LOGN2>
-static void ntt_rows_launch(bool inv, const LimbSet &in, const LimbSet &out)
+static bool ntt_rows_launch(bool inv, const LimbSet &in, const LimbSet &out, const uint64_t *post = nullptr)
 {
   const unsigned logn = G.logn, n = G.n;
   const unsigned blocks = in.count * (n / 4096);
@@ -494,9 +520,12 @@ static void ntt_rows_launch(bool inv, const LimbSet &in, const LimbSet &out)
     // with them and keeps 16-byte (w, w/q) entries
     // inverse: each thread loads its round-C words directly (16-byte loads,
     // no transpose through LDS): 94.6 -> 88.4-90.5 us per 48-poly group
-    auto k = inv ? ntt_rows_q_kernel<LOGN2, true, QN, true, true> : ntt_rows_q_kernel<LOGN2, false, QN>;
+    auto k = inv ? (post ? ntt_rows_q_kernel<LOGN2, true, QN, true, true, true> : ntt_rows_q_kernel<LOGN2, true, QN, true, true>)
+                 : ntt_rows_q_kernel<LOGN2, false, QN>;
     hipLaunchKernelGGL(k, dim3(xcd_blocks(members, groups)), dim3(256 * QN), 0, G.stream, in, out, logn, tw, G.dev.mc,
-                       members);
+                       members, post);
+  } else if (post) {
+    return false;  // (the batched form only)
   } else if (inv) {
     hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, true>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
                        G.dev.mc);
@@ -504,6 +533,7 @@ static void ntt_rows_launch(bool inv, const LimbSet &in, const LimbSet &out)
     hipLaunchKernelGGL((ntt3_rows_kernel<LOGN2, false>), dim3(2 * blocks), dim3(256), 0, G.stream, in, out, logn, tw,
                        G.dev.mc);
   }
+  return true;
 }
 
 template <int LOGT1, int LOGN2>
@@ -3772,7 +3802,9 @@ __global__ void __launch_bounds__(256, 2) dn_cols_kernel(const uint64_t *X, size
 // Forward row pass of conv on 8-element row tiles with the combine as its
 // epilogue.  The epilogue operand X_t is fetched at kernel start so its
 // latency overlaps the row pass.  (The key switch added P (d0, d1) to X.)
-template <int LOGN2>
+// PRE: conv is pre-scaled (dn_cols' pre form: conv' = conv [D^-1]_t), so
+// out = X [D^-1]_t - rowNTT(conv'), the same residue.
+template <int LOGN2, bool PRE = false>
 __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint64_t *out, size_t out_pstride,
                                                        const uint64_t *X, size_t x_pstride, unsigned logn,
                                                        unsigned lvl, unsigned L, unsigned npoly, DownTable tab,
@@ -3819,7 +3851,9 @@ __global__ void __launch_bounds__(256) dn_rows_kernel(const uint64_t *conv, uint
   for (int i = 0; i < 8; i++) {
     const int e = wl_elem(i);
     const uint64_t c = lds[T::wl(th, i)];
-    if (q < F64_QMAX) {
+    if constexpr (PRE) {
+      o[e] = sub_mod(mulc_canon(xv[i], dinv, dinvp, q), c, q);
+    } else if (q < F64_QMAX) {
       // exact FP64 product: |X - conv| < q, the product < 1.25 q
       const double qd = (double)q, qinv = 1.0 / qd, di = f64_from_u52(dinv);
       o[e] = f64_canon(f64_mulmod(f64_from_u52(xv[i]) - f64_from_u52(c), di, di * qinv, qd), qd, qinv);
@@ -3871,20 +3905,48 @@ static void dn_cols_stage(uint64_t *conv, const uint64_t *X, size_t x_pstride, s
 
 template <int LOGT1, int LOGN2>
 static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, const uint64_t *X, size_t x_pstride,
-                            unsigned npoly, unsigned lvl, const DownTable &tab)
+                            unsigned npoly, unsigned lvl, const DownTable &tab, bool pre)
 {
   const unsigned n = G.n, keep = tab.keep;
   const Tw2 tw{G.tw2, G.itw2, G.twd, G.itwd};
-  dn_cols_stage<LOGT1>(conv, X, x_pstride, (size_t)keep << G.logn, npoly, lvl, tab, false);
+  dn_cols_stage<LOGT1>(conv, X, x_pstride, (size_t)keep << G.logn, npoly, lvl, tab, pre);
   // reads conv and X, writes out
   ProfScope ps(KC_DN_ROWS, 8.0 * n * npoly * keep * 3.0);
-  hipLaunchKernelGGL((dn_rows_kernel<LOGN2>), dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv,
-                     out, out_pstride, X, x_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
+  hipLaunchKernelGGL((pre ? dn_rows_kernel<LOGN2, true> : dn_rows_kernel<LOGN2, false>),
+                     dim3(xcd_blocks(npoly, keep * (n / 2048))), dim3(256), 0, G.stream, conv, out, out_pstride, X,
+                     x_pstride, G.logn, lvl, G.L, npoly, tab, tw, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
+// The inverse row pass of the dropped limbs dr before k_moddown_fused, each
+// word times n^-1 [(D/d)^-1]_d (the DownTable's ysc): then the fused ModDown
+// takes the pre-scaled column kernels (pre = true), as the split key switch's
+// dropped slots do.  False (nothing launched) when the batched row form does
+// not apply: then k_ntt_rows and pre = false.
+bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode)
+{
+  static const bool on = !(getenv("GPQHE_DN_PRE") && atoi(getenv("GPQHE_DN_PRE")) == 0);
+  const DownTable &tab = down_table(lvl, mode);
+  if (!on || !dr.count || dr.per != tab.nd || dr.ngp)
+    return false;
+  bool ok;
+  {
+    ProfScope ps(KC_NTT3_ROWS_INV, 16.0 * G.n * dr.count);
+    switch (G.logn) {
+    case 13: ok = ntt_rows_launch<7>(true, dr, dr, tab.ysc); break;
+    case 14: ok = ntt_rows_launch<7>(true, dr, dr, tab.ysc); break;
+    case 15: ok = ntt_rows_launch<8>(true, dr, dr, tab.ysc); break;
+    case 16: ok = ntt_rows_launch<8>(true, dr, dr, tab.ysc); break;
+    case 17: ok = ntt_rows_launch<9>(true, dr, dr, tab.ysc); break;
+    default: ok = false;
+    }
+  }
+  HIP_CHECK(hipGetLastError());
+  return ok;
+}
+
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode)
+                     int mode, bool pre)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
@@ -3893,11 +3955,11 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
     gpqhe_die("fused ModDown over %u moduli unsupported (max 5)", tab.nd);
   uint64_t *conv = (uint64_t *)pool_alloc((size_t)npoly * tab.keep * G.n * 8);
   switch (G.logn) {
-  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
-  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
-  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
-  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
-  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab); break;
+  case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
+  case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
+  case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
+  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
+  case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
   pool_free(conv);

@@ -401,6 +401,18 @@ __device__ __forceinline__ double fbc_term(double y, double c, double cq, double
 #endif
 
 constexpr uint64_t F64_QMAX = 1ull << 51;  // ArF64 applies to moduli below this
+
+// x w mod q, canonical, for canonical x and a constant w < q with its Shoup
+// companion wp: the exact FP64 product below F64_QMAX (as dn_rows_kernel's
+// epilogue), 64-bit Shoup above
+__device__ __forceinline__ uint64_t mulc_canon(uint64_t x, uint64_t w, uint64_t wp, uint64_t q)
+{
+  if (q < F64_QMAX) {
+    const double qd = (double)q, qinv = 1.0 / qd, wd = f64_from_u52(w);
+    return f64_canon(f64_mulmod(f64_from_u52(x), wd, wd * qinv, qd), qd, qinv);
+  }
+  return mul_shoup(x, w, wp, q);
+}
 constexpr uint64_t F64_LAZY = 1ull << 50;  // and its lazy stage reduction below this
 
 // Forward row passes with the twiddles of one row tile staged in LDS.  A
