@@ -283,9 +283,6 @@ struct EwProg {
   static constexpr unsigned MAX = 16;
   EwOp op[MAX];
   unsigned count;
-  // set by k_ew_prog: operand a / b of op j is op src[j]'s result (>= 0,
-  // forwarded in registers) or read from memory (-1)
-  int8_t sa[MAX], sb[MAX];
 };
 void k_ew_prog(const EwProg &p);
 // k_ew_prog(p), then he_dcd of the NTT-form plaintext pt (nl <= 2 limbs,

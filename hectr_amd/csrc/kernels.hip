@@ -1051,128 +1051,14 @@ __global__ void ew_prog_kernel(EwProg pr, unsigned logn, const ModConst *mc)
   }
 }
 
-// The same program with every intermediate forwarded in registers
-// (ew_fwd_plan): all memory operands are loaded first, one round trip, then
-// the ops run in order on registers, then every output is stored in order.
-// In ew_prog_kernel each op's loads wait for the previous op's store (it may
-// alias them): one memory round trip per op.
-__global__ void __launch_bounds__(256) ew_prog_fwd_kernel(EwProg pr, unsigned logn, const ModConst *mc)
-{
-  constexpr unsigned M = EwProg::MAX;
-  const size_t n = (size_t)1 << logn;
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n)
-    return;
-  const unsigned l = blockIdx.y;
-  const ModConst m = mc[l];
-  const size_t off = ((size_t)l << logn) + i;
-  uint64_t ra[M], rb[M], rs[M], r[M];
-#pragma unroll
-  for (unsigned j = 0; j < M; j++) {
-    ra[j] = rb[j] = rs[j] = r[j] = 0;
-    if (j < pr.count && l < pr.op[j].lvl) {
-      const EwOp &o = pr.op[j];
-      if (pr.sa[j] < 0)
-        ra[j] = o.a[off];
-      if ((o.kind == EW_ADD || o.kind == EW_SUB || o.kind == EW_DEC) && pr.sb[j] < 0)
-        rb[j] = o.b[off];
-      if (o.kind == EW_DEC)
-        rs[j] = o.s[off];
-    }
-  }
-#pragma unroll
-  for (unsigned j = 0; j < M; j++) {
-    if (j < pr.count && l < pr.op[j].lvl) {
-      const EwOp &o = pr.op[j];
-      uint64_t x = ra[j], y = rb[j];
-#pragma unroll
-      for (unsigned k = 0; k < j; k++) {  // (uniform selects)
-        if (pr.sa[j] == (int)k)
-          x = r[k];
-        if (pr.sb[j] == (int)k)
-          y = r[k];
-      }
-      switch (o.kind) {
-      case EW_ADD:
-        r[j] = add_mod(x, y, m.q);
-        break;
-      case EW_SUB:
-        r[j] = sub_mod(x, y, m.q);
-        break;
-      case EW_NEG:
-        r[j] = neg_mod(x, m.q);
-        break;
-      case EW_DEC:
-        r[j] = add_mod(x, mul_mod(y, rs[j], m), m.q);
-        break;
-      default:
-        r[j] = x;
-      }
-    }
-  }
-#pragma unroll
-  for (unsigned j = 0; j < M; j++)
-    if (j < pr.count && l < pr.op[j].lvl)
-      pr.op[j].out[off] = r[j];
-}
-
-// Register forwarding plan of p (sa / sb), or false when some memory operand
-// overlaps an earlier op's output other than as exactly that output with at
-// least the reader's limbs (then the op-by-op kernel runs).
-static bool ew_fwd_plan(EwProg &p)
-{
-  static const bool on = !(getenv("GPQHE_EW_FWD") && atoi(getenv("GPQHE_EW_FWD")) == 0);
-  if (!on)
-    return false;
-  const size_t n = G.n;
-  auto overlap = [&](const uint64_t *a, unsigned la, const uint64_t *b, unsigned lb) {
-    return a < b + (size_t)lb * n && b < a + (size_t)la * n;
-  };
-  for (unsigned j = 0; j < p.count; j++) {
-    const EwOp &o = p.op[j];
-    const bool hb = o.kind == EW_ADD || o.kind == EW_SUB || o.kind == EW_DEC;
-    auto plan = [&](const uint64_t *x, int8_t &src) {
-      src = -1;
-      for (int k = (int)j - 1; k >= 0; k--) {
-        if (p.op[k].out == x) {  // the latest writer of exactly x
-          if (p.op[k].lvl < o.lvl)
-            return false;
-          src = (int8_t)k;
-          return true;
-        }
-        if (overlap(p.op[k].out, p.op[k].lvl, x, o.lvl))
-          return false;
-      }
-      return true;
-    };
-    if (!plan(o.a, p.sa[j]))
-      return false;
-    if (hb && !plan(o.b, p.sb[j]))
-      return false;
-    if (!hb)
-      p.sb[j] = -1;
-    if (o.kind == EW_DEC) {  // the key: never an output of the program
-      for (unsigned k = 0; k < p.count; k++)
-        if (overlap(p.op[k].out, p.op[k].lvl, o.s, o.lvl))
-          return false;
-    }
-  }
-  return true;
-}
-
-void k_ew_prog(const EwProg &p0)
+void k_ew_prog(const EwProg &p)
 {
   unsigned lv = 0;
-  for (unsigned j = 0; j < p0.count; j++)
-    lv = std::max(lv, p0.op[j].lvl);
+  for (unsigned j = 0; j < p.count; j++)
+    lv = std::max(lv, p.op[j].lvl);
   if (!lv)
     return;
-  EwProg p = p0;
-  if (ew_fwd_plan(p))
-    hipLaunchKernelGGL(ew_prog_fwd_kernel, dim3((G.n + TPB - 1) / TPB, lv), dim3(TPB), 0, G.stream, p, G.logn,
-                       G.dev.mc);
-  else
-    hipLaunchKernelGGL(ew_prog_kernel, dim3((G.n + TPB - 1) / TPB, lv), dim3(TPB), 0, G.stream, p, G.logn, G.dev.mc);
+  hipLaunchKernelGGL(ew_prog_kernel, dim3((G.n + TPB - 1) / TPB, lv), dim3(TPB), 0, G.stream, p, G.logn, G.dev.mc);
   HIP_CHECK(hipGetLastError());
 }
 
