@@ -1671,6 +1671,10 @@ __global__ void enc_batch_m_kernel(EncBatch bt, EncM em, const uint64_t *vee, co
   const ModConst m = mc[l];
   const size_t o = ((size_t)l << logn) + i, w = (size_t)lvl << logn;
   const uint64_t *v = vee + 3 * e * w;
+  // the combine's noise and key words requested before the evaluation, whose
+  // serial products they would otherwise wait behind (lane 0: e0, pk0; lane
+  // 1: e1, pk1; lanes 2, 3 read lane 1's words, unused)
+  const uint64_t nv = v[o], ne = v[(b == 0 ? 1 : 2) * w + o], nk = (b == 0 ? pk0 : pk1)[o];
   uint64_t mh = 0;
   const int r = em.row_of[e];
   if (r >= 0) {  // (uniform)
@@ -1693,9 +1697,9 @@ __global__ void enc_batch_m_kernel(EncBatch bt, EncM em, const uint64_t *vee, co
     mh = bt.m[e][o];
   }
   if (b == 0)
-    bt.c0[e][o] = add_mod(add_mod(v[w + o], mul_mod(v[o], pk0[o], m), m.q), mh, m.q);
+    bt.c0[e][o] = add_mod(add_mod(ne, mul_mod(nv, nk, m), m.q), mh, m.q);
   else if (b == 1)
-    bt.c1[e][o] = add_mod(v[2 * w + o], mul_mod(v[o], pk1[o], m), m.q);
+    bt.c1[e][o] = add_mod(ne, mul_mod(nv, nk, m), m.q);
 }
 
 void k_enc_combine_m(const EncBatch &b, const EncM &em, unsigned k, const uint64_t *vee, const uint64_t *pk0,

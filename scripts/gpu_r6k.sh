@@ -16,7 +16,9 @@ fi
 V=${AB_VAR:-GPQHE_SPEC_MODUP_SPLIT}
 for r in $(seq 1 ${ROUNDS:-3}); do
   for v in 1 0; do
-    env $V=$v timeout -k 10 200 python -c "
+    # AB_VAR=GPQHE_LIB: 1 = the working tree's library, 0 = hectr_amd/lib_ab's
+    if [ "$V" = GPQHE_LIB ]; then E="GPQHE_LIB=$([ $v = 1 ] && echo hectr_amd/lib || echo hectr_amd/lib_ab)/libgpqhe.so"; else E="$V=$v"; fi
+    env $E timeout -k 10 200 python -c "
 import sys; sys.path.insert(0, '.'); import bench, json
 d = bench.cstr_c_caller(reps=5)
 c4 = d.get('config4_c_driver', {})
