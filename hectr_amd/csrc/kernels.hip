@@ -3940,7 +3940,8 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
 // not apply: then k_ntt_rows and pre = false.
 bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode)
 {
-  static const bool on = !(getenv("GPQHE_DN_PRE") && atoi(getenv("GPQHE_DN_PRE")) == 0);
+  const char *sw = getenv("GPQHE_DN_PRE");  // (read per call: tests switch it in-process)
+  const bool on = !(sw && atoi(sw) == 0);
   const DownTable &tab = down_table(lvl, mode);
   if (!on || !dr.count || dr.per != tab.nd || dr.ngp)
     return false;

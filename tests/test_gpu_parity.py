@@ -667,7 +667,7 @@ def test_rekey_between_speculative_steps(oracle, product):
 
 @pytest.mark.parametrize("switch", ["GPQHE_SPEC", "GPQHE_SPEC_ATTACH", "GPQHE_SPEC_EARLY", "GPQHE_DEFER",
                                     "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV", "GPQHE_SPEC_ATTACH_TAKE",
-                                    "GPQHE_SPEC_GEMV"])
+                                    "GPQHE_SPEC_GEMV", "GPQHE_SPEC_MODUP_SPLIT"])
 def test_small_n_switch_off_paths(switch):
     """Each small-N switch is read once per process (api.cpp static const), so
     its off path runs in a child process (one at a time, nothing else on the

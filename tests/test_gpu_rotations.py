@@ -179,6 +179,29 @@ def test_gemv_batch_few_diagonals(oracle, product, name, diags):
         e.free_evks(k[2])
 
 
+@pytest.mark.parametrize("name", ["bench51", "bench_d2"])
+def test_gemv_rot_batch_dn_pre_off(oracle, product, monkeypatch, name):
+    """GPQHE_DN_PRE=0: the ModDown of he_gemv_batch / he_rot_batch on the
+    generic column kernel with the scale after its inverse column pass,
+    instead of the pre-scaled row pass + dn_colsf form -- the
+    same residues as the oracle either way."""
+    init_slots(oracle, product, name, 16, seed=43)
+    s, n, lvl, cnt = 16, product.n, 8, 3
+    ko, kp = rot_keys(oracle), rot_keys(product)
+    rng = np.random.default_rng(7)
+    zs = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
+    Mc = np.ascontiguousarray(sample_matrix(s, 5).ravel(), dtype=np.complex128)
+    host = encrypt_batch(product, kp[0], zs, nlimbs=lvl)
+    monkeypatch.setenv("GPQHE_DN_PRE", "0")
+    want, got = run_batch(oracle, product, ko[2], kp[2], "he_gemv_batch", host, cnt * 2 * (lvl - 1) * n,
+                          Mc.ctypes.data, "IN", cnt, lvl)
+    assert np.array_equal(got, want), f"gemv: {np.count_nonzero(got != want)} residues differ"
+    want, got = run_batch(oracle, product, ko[2], kp[2], "he_rot_batch", host, cnt * 2 * lvl * n, "IN", cnt, lvl, 2)
+    assert np.array_equal(got, want), f"rot: {np.count_nonzero(got != want)} residues differ"
+    for e, k in ((oracle, ko), (product, kp)):
+        e.free_evks(k[2])
+
+
 def test_gemv_rot_batch_chunks_and_empty(oracle, product, monkeypatch):
     """The batch path's chunk loop (GPQHE_GEMV_CHUNK=2: 5 ciphertexts as
     2 + 2 + 1, the workspace and orbit table per chunk) against the oracle, and
