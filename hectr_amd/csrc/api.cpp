@@ -328,6 +328,231 @@ extern "C" unsigned gpqhe_spec_gemv_taken(void)
   return g_sg_taken;
 }
 
+// Speculative decode of the small-N step (SpecDcd; GPQHE_SPEC_DCD=0 turns it
+// off).  A step's tail -- the queued elementwise program (HECTR's he_add,
+// he_neg, he_copy_ct, he_add, he_dec: src/hempc.c:261-266, src/ctr.c:486) and
+// the decode -- waits on the caller: it is issued at he_dcd, after the
+// caller's own host work.  Its operands are this step's speculated gemv
+// results, its encryptions, its own temporaries and the secret key, so the
+// last step's program, recorded by the roles of its operands (SdPat), is
+// replayed on this step's objects right after the speculated gemvs (temporaries
+// in scratch, the decode into pinned memory), where it runs in the caller's
+// shadow.  he_dcd takes the replay's values when this step's program has the
+// same pattern, reading the same blocks (the gemv results still in the blocks
+// the speculation wrote, the encryptions still holding their streams:
+// C1Prov), and the real program then runs without being waited for.  When the
+// replay is still running at he_dcd on two consecutive steps (the caller
+// outruns the device: the replay only adds work to the step's chain) it stops.
+static unsigned env_u(const char *name, unsigned dflt);
+enum : uint8_t { SR_OUT = 0, SR_Y = 1, SR_ENC = 2 };
+struct SdRole {
+  uint8_t kind = 0, idx = 0, poly = 0;
+  bool operator==(const SdRole &o) const { return kind == o.kind && idx == o.idx && poly == o.poly; }
+};
+struct SdPat {
+  unsigned count = 0, nl = 0, slots = 0, sid = 0;  // sid: the out id holding the decoded plaintext
+  double scale = 0;
+  const uint64_t *sk = nullptr;
+  uint32_t kind[EwProg::MAX] = {}, lvl[EwProg::MAX] = {};
+  SdRole out[EwProg::MAX], a[EwProg::MAX], b[EwProg::MAX];
+  bool same(const SdPat &o) const
+  {
+    if (count != o.count || nl != o.nl || slots != o.slots || sid != o.sid || scale != o.scale || sk != o.sk)
+      return false;
+    for (unsigned j = 0; j < count; j++)
+      if (kind[j] != o.kind[j] || lvl[j] != o.lvl[j] || !(out[j] == o.out[j]) || !(a[j] == o.a[j]) ||
+          !(b[j] == o.b[j]))
+        return false;
+    return true;
+  }
+};
+struct SdCtx {  // a step's role blocks (spec_gemv_launch)
+  const uint64_t *y[GemvJobs::MAX] = {};
+  unsigned ny = 0, ylvl = 0;
+  const uint64_t *e[GPQHE_MAXGRP][2] = {};
+  uint64_t es[GPQHE_MAXGRP] = {};
+  unsigned ne = 0, elvl = 0;
+  bool valid = false;
+};
+struct SpecDcd {
+  SdPat pat;  // the pattern replayed this step
+  uint64_t *scratch = nullptr, *cws = nullptr;
+  size_t swords = 0, cwords = 0;
+  void *z = nullptr;  // pinned decoded values
+  size_t zbytes = 0;
+  hipEvent_t ev = nullptr;
+  bool valid = false;
+};
+static SdCtx g_sd_ctx;    // this step's roles
+static SdPat g_sd_next;   // this step's pattern, replayed by the next step
+static bool g_sd_next_ok = false;
+static SpecDcd g_sd;
+static unsigned g_sd_taken = 0, g_sd_late = 0;
+static bool g_sd_off = false;
+
+extern "C" unsigned gpqhe_spec_dcd_taken(void)
+{
+  return g_sd_taken;
+}
+
+// The roles of program p's operands and of the decoded plaintext ptd under the
+// step roles c; false when some operand has none (or could alias one).
+static bool sd_pattern(const EwProg &p, const uint64_t *ptd, unsigned nl, unsigned slots, double scale,
+                       const SdCtx &c, SdPat &r)
+{
+  if (!c.valid || !p.count || nl < 1 || nl > 2)
+    return false;
+  const size_t n = G.n, ypw = (size_t)G.L << G.logn;
+  r = SdPat{};
+  r.count = p.count;
+  r.nl = nl;
+  r.slots = slots;
+  r.scale = scale;
+  auto ov = [&](const uint64_t *x, unsigned lx, const uint64_t *y, unsigned ly) {
+    return x < y + (size_t)ly * n && y < x + (size_t)lx * n;
+  };
+  unsigned oid[EwProg::MAX];
+  // operand x read over lv limbs before op j: the latest earlier writer of
+  // exactly x (with at least those limbs), else a role block
+  auto read = [&](unsigned j, const uint64_t *x, unsigned lv, SdRole &role) {
+    for (int k = (int)j - 1; k >= 0; k--) {
+      const EwOp &w = p.op[k];
+      if (w.out == x) {
+        if (w.lvl < lv)
+          return false;
+        role = SdRole{SR_OUT, (uint8_t)oid[k], 0};
+        return true;
+      }
+      if (ov(w.out, w.lvl, x, lv))
+        return false;
+    }
+    for (unsigned i = 0; i < c.ny; i++)
+      for (unsigned q = 0; q < 2; q++)
+        if (x == c.y[i] + q * ypw) {
+          if (lv > c.ylvl)
+            return false;
+          role = SdRole{SR_Y, (uint8_t)i, (uint8_t)q};
+          return true;
+        }
+    for (unsigned o = 0; o < c.ne; o++)
+      for (unsigned q = 0; q < 2; q++)
+        if (x == c.e[o][q]) {
+          if (lv > c.elvl)
+            return false;
+          role = SdRole{SR_ENC, (uint8_t)o, (uint8_t)q};
+          return true;
+        }
+    return false;
+  };
+  for (unsigned j = 0; j < p.count; j++) {
+    const EwOp &o = p.op[j];
+    r.kind[j] = o.kind;
+    r.lvl[j] = o.lvl;
+    oid[j] = j;
+    for (unsigned k = 0; k < j; k++) {
+      if (p.op[k].out == o.out) {
+        oid[j] = oid[k];
+        break;
+      }
+      if (ov(p.op[k].out, p.op[k].lvl, o.out, o.lvl))
+        return false;
+    }
+    r.out[j] = SdRole{SR_OUT, (uint8_t)oid[j], 0};
+    if (!read(j, o.a, o.lvl, r.a[j]))
+      return false;
+    if ((o.kind == EW_ADD || o.kind == EW_SUB || o.kind == EW_DEC) && !read(j, o.b, o.lvl, r.b[j]))
+      return false;
+    if (o.kind == EW_DEC) {  // the key: one block, never an output
+      if (r.sk && r.sk != o.s)
+        return false;
+      r.sk = o.s;
+      for (unsigned k = 0; k < p.count; k++)
+        if (ov(p.op[k].out, p.op[k].lvl, o.s, o.lvl))
+          return false;
+    }
+  }
+  SdRole pr;
+  if (!read(p.count, ptd, nl, pr) || pr.kind != SR_OUT)
+    return false;
+  r.sid = pr.idx;
+  return true;
+}
+
+// Every encryption role of r still holds its stream (C1Prov: any write since
+// dropped it).
+static bool sd_enc_fresh(const SdPat &r, const SdCtx &c)
+{
+  auto ok = [&](const SdRole &q) {
+    if (q.kind != SR_ENC)
+      return true;
+    auto it = g_prov.find(c.e[q.idx][q.poly]);
+    return it != g_prov.end() && !it->second.sub && it->second.c0 == (q.poly == 0) && it->second.sa == c.es[q.idx] &&
+           it->second.lvl == c.elvl;
+  };
+  for (unsigned j = 0; j < r.count; j++)
+    if (!ok(r.a[j]) || !ok(r.b[j]))
+      return false;
+  return true;
+}
+
+// The last step's pattern on this step's roles (g_sd_ctx): the program with
+// its temporaries in scratch, then the decode into pinned memory.
+static void sd_replay(const SdPat &r)
+{
+  const size_t blk = (size_t)G.L << G.logn, ypw = blk;
+  unsigned nid = 0;
+  for (unsigned j = 0; j < r.count; j++)
+    nid = std::max(nid, (unsigned)r.out[j].idx + 1);
+  const SdCtx &c = g_sd_ctx;
+  auto ptr = [&](const SdRole &q) -> const uint64_t * {
+    if (q.kind == SR_OUT)
+      return q.idx < nid ? g_sd.scratch + q.idx * blk : nullptr;
+    if (q.kind == SR_Y)
+      return q.idx < c.ny ? c.y[q.idx] + q.poly * ypw : nullptr;
+    return q.idx < c.ne ? c.e[q.idx][q.poly] : nullptr;
+  };
+  if (g_sd.swords < nid * blk) {
+    pool_free(g_sd.scratch);  // stream-ordered: its last reader was launched before
+    g_sd.scratch = (uint64_t *)pool_alloc(nid * blk * 8);
+    g_sd.swords = nid * blk;
+  }
+  if (g_sd.cwords < ((size_t)r.nl << G.logn)) {
+    pool_free(g_sd.cws);
+    g_sd.cws = (uint64_t *)pool_alloc(((size_t)r.nl << G.logn) * 8);
+    g_sd.cwords = (size_t)r.nl << G.logn;
+  }
+  EwProg p{};
+  p.count = r.count;
+  for (unsigned j = 0; j < r.count; j++) {
+    const bool hb = r.kind[j] == EW_ADD || r.kind[j] == EW_SUB || r.kind[j] == EW_DEC;
+    const uint64_t *a = ptr(r.a[j]), *b = hb ? ptr(r.b[j]) : nullptr;
+    if (!a || (hb && !b) || r.out[j].idx >= nid)
+      return;
+    p.op[j] = EwOp{g_sd.scratch + r.out[j].idx * blk, a, b, r.kind[j] == EW_DEC ? r.sk : nullptr, r.kind[j], r.lvl[j]};
+  }
+  const size_t zb = (size_t)r.slots * 16;
+  if (g_sd.zbytes < zb) {
+    if (g_sd.z)
+      HIP_CHECK(hipHostFree(g_sd.z));
+    HIP_CHECK(hipHostMalloc(&g_sd.z, zb, hipHostMallocDefault));
+    g_sd.zbytes = zb;
+  }
+  void *zd = nullptr;
+  HIP_CHECK(hipHostGetDevicePointer(&zd, g_sd.z, 0));
+  if (!g_sd.ev)
+    HIP_CHECK(hipEventCreateWithFlags(&g_sd.ev, hipEventDisableTiming));
+  k_ew_decode(p, (double *)zd, g_sd.scratch + r.sid * blk, r.nl, r.slots, r.scale, g_sd.cws);
+  HIP_CHECK(hipEventRecord(g_sd.ev, G.stream));
+  g_sd.pat = r;
+  g_sd.valid = true;
+}
+
+static bool sd_on()
+{
+  static const bool on = env_u("GPQHE_SPEC_DCD", 1) != 0;
+  return on && !g_sd_off;
+}
+
 static void prov_forget(const void *obj_data, size_t pstride_words)
 {
   if (g_prov.empty() || !obj_data)
@@ -386,6 +611,7 @@ static void check_ctx()
   g_prov.clear();
   g_smu.valid = false;
   g_smu_next.pending = false;
+  g_sd.valid = false;
   flush_ew();
   if (!g_pgemv.empty())
     flush_gemvs();
@@ -854,6 +1080,15 @@ extern "C" void hectx_exit(void)
     HIP_CHECK(hipEventDestroy(g_dcd_ev));
     g_dcd_ev = nullptr;
   }
+  if (g_sd.ev)
+    HIP_CHECK(hipEventDestroy(g_sd.ev));
+  if (g_sd.z)
+    HIP_CHECK(hipHostFree(g_sd.z));
+  g_sd = SpecDcd{};  // (its scratch blocks go with the pool)
+  g_sd_ctx = SdCtx{};
+  g_sd_next_ok = false;
+  g_sd_taken = g_sd_late = 0;
+  g_sd_off = false;
   k_prof_release();
   gemv_cache_clear();
   fold_cache_clear();
@@ -1213,6 +1448,8 @@ static void flush_pending()
     if (i0 == 0) {
       g_spec_pats_next.clear();  // a new step: its gemv inputs are recorded afresh
       g_sg_next.clear();
+      g_sd_ctx.valid = false;
+      g_sd.valid = false;
     }
     for (unsigned e = 0; e < k; e++) {
       g_prov[enc[i0 + e].c1] = C1Prov{enc[i0 + e].stream, 0, enc[i0 + e].pk1, lvl, false};
@@ -1584,6 +1821,23 @@ static void spec_gemv_launch(const std::vector<PendEnc> &enc, const std::vector<
   g_sg.np = np;
   g_sg.lvl = lvl;
   g_sg.valid = true;
+  // this step's role blocks, and the last step's tail replayed on them (SpecDcd)
+  g_sd_ctx = SdCtx{};
+  for (unsigned i = 0; i < np; i++)
+    g_sd_ctx.y[i] = g_sg.Y[i];
+  g_sd_ctx.ny = np;
+  g_sd_ctx.ylvl = lvl - 1;
+  for (unsigned o = 0; o < enc.size() && o < GPQHE_MAXGRP; o++) {
+    g_sd_ctx.e[o][0] = enc[o].c0;
+    g_sd_ctx.e[o][1] = enc[o].c1;
+    g_sd_ctx.es[o] = enc[o].stream;
+    g_sd_ctx.ne = o + 1;
+  }
+  g_sd_ctx.elvl = lvl;
+  g_sd_ctx.valid = true;
+  g_sd.valid = false;
+  if (g_sd_next_ok && sd_on())
+    sd_replay(g_sd_next);
 }
 
 extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int slots)
@@ -1595,6 +1849,35 @@ extern "C" void he_dcd_ex(gpqhe_complex_t z[], const he_pt_t *pt, unsigned int s
     // the small-N step's tail: the queued elementwise program (he_add, he_neg,
     // he_copy_ct, he_add, he_dec), then the inverse transform and the decoder
     // in one more launch (k_ew_decode)
+    // this step's tail pattern (replayed next step), and the replay of the
+    // last step's (SpecDcd) when this step's is the same
+    SdPat cur;
+    const bool quiet = g_pgemv.empty() && g_pecd.empty() && g_penc.empty();
+    g_sd_next_ok = quiet && sd_pattern(g_pew, pt->data, pt->nlimbs, slots, pt->scale, g_sd_ctx, cur);
+    if (g_sd_next_ok)
+      g_sd_next = cur;
+    if (g_sd.valid && g_sd_next_ok && g_spec_early && cur.same(g_sd.pat) && sd_enc_fresh(cur, g_sd_ctx)) {
+      g_sd.valid = false;
+      flush_ew();  // the real program: its objects, not waited for
+      g_spec_early = false;
+      if (g_smu_next.pending)
+        spec_modup_launch();
+      const hipError_t q = hipEventQuery(g_sd.ev);
+      (void)hipGetLastError();  // (not ready is no error)
+      if (q != hipSuccess) {
+        // the device behind the caller: the replay only lengthens the chain
+        // (GPQHE_SPEC_DCD=2 keeps it on: tests)
+        if (++g_sd_late >= 2 && env_u("GPQHE_SPEC_DCD", 1) != 2)
+          g_sd_off = true;
+      } else {
+        g_sd_late = 0;
+      }
+      HIP_CHECK(hipEventSynchronize(g_sd.ev));
+      memcpy(z, g_sd.z, zb);
+      g_sd_taken++;
+      return;
+    }
+    g_sd.valid = false;
     if (!g_pgemv.empty())
       flush_gemvs();
     if (!g_pecd.empty() || !g_penc.empty())

@@ -139,11 +139,12 @@ SIGNATURES = {
     "gpqhe_prof_enable": (None, [C.c_int]),
     "gpqhe_prof_collect": (C.c_uint, [P(KStat), C.c_uint]),
     "gpqhe_spec_gemv_taken": (C.c_uint, []),
+    "gpqhe_spec_dcd_taken": (C.c_uint, []),
 }
 
 #: [ext] symbols added in round 6: a library named by GPQHE_LIB (an A/B
 #: baseline built from an older commit) may lack them
-NEWER = {"gpqhe_spec_gemv_taken"}
+NEWER = {"gpqhe_spec_gemv_taken", "gpqhe_spec_dcd_taken"}
 
 #: symbols declared in include/gpqhe.h (checked by tests/test_abi.py)
 EXPORTED = sorted(SIGNATURES)

@@ -240,6 +240,9 @@ unsigned gpqhe_prof_collect(gpqhe_kstat_t *out, unsigned max);
 /* [ext] he_gemv calls served by the speculated gemv of the small-N step     */
 /* (api.cpp SpecGemv) since hectx_init; the oracle returns 0.                */
 unsigned gpqhe_spec_gemv_taken(void);
+/* [ext] he_dcd calls of the small-N step served by the replay of the last   */
+/* step's elementwise tail and decode (api.cpp SpecDcd); the oracle: 0.      */
+unsigned gpqhe_spec_dcd_taken(void);
 
 /* ------------------------------------------------------------------------ */
 /* [ext] Serialization (host buffers): residues in the payload layout above, */

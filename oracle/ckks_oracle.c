@@ -460,8 +460,13 @@ void gpqhe_sync(void)
 {
 }
 
-/* no speculation here: every he_gemv runs as called */
+/* no speculation here: every he_gemv and he_dcd runs as called */
 unsigned gpqhe_spec_gemv_taken(void)
+{
+  return 0;
+}
+
+unsigned gpqhe_spec_dcd_taken(void)
 {
   return 0;
 }

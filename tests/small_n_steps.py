@@ -152,7 +152,7 @@ def rekeyed_steps(e, seed=1234, rng_seed=41):
     return res
 
 
-def speculative_gemvs(e, seed=1234, rng_seed=53):
+def speculative_gemvs(e, seed=1234, rng_seed=53, plan=None):
     """HECTR's step with its own call order (all five encodes, all five
     encryptions, the plaintexts freed: src/ctr.c:461-480, which starts the
     early combine and, from the third step on, the speculated gemvs of the
@@ -167,8 +167,8 @@ def speculative_gemvs(e, seed=1234, rng_seed=53):
     M1 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
     M2 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
     M3 = (rng.uniform(-1, 1, (s, s)) + 0j).astype(np.complex128)
-    plan = ["same", "same", "same", "newM", "same", "swap", "same", "clobber", "same", "order", "same", "regen",
-            "same", "one", "same", "same"]
+    plan = plan or ["same", "same", "same", "newM", "same", "swap", "same", "clobber", "same", "order", "same",
+                    "regen", "same", "one", "same", "same"]
     zs = [[rng.uniform(-1, 1, s) + 0j for _ in range(5)] for _ in plan]
     pk, sk, rk = keys(e, rot=True)
     res, keep = [], []

@@ -655,6 +655,27 @@ def test_speculative_gemvs(oracle, product):
     assert taken >= 10, taken
 
 
+def test_speculative_decode(oracle, product, monkeypatch):
+    """The replayed tail of the small-N step (api.cpp SpecDcd: the last step's
+    elementwise program and decode on this step's speculated gemvs): runs of
+    HECTR's step in its own call order, broken by steps whose program or
+    operands differ (a changed matrix, an encryption overwritten before its
+    he_sub, the gemvs in the other order, one gemv), where the replay must not
+    be taken -- every decoded value and object bit-exact vs the oracle, and the
+    product served decodes from the replay."""
+    from tests.small_n_steps import mismatches, speculative_gemvs
+    plan = ["same"] * 7 + ["newM", "same", "same", "same", "clobber"] + ["same"] * 4 + ["order"] + ["same"] * 4 + \
+        ["one"] + ["same"] * 4
+    # (a Python caller outruns the device: keep the replay on, which the
+    # library otherwise stops after two late steps)
+    monkeypatch.setenv("GPQHE_SPEC_DCD", "2")
+    want = speculative_gemvs(oracle, plan=plan)
+    got = speculative_gemvs(product, plan=plan)
+    dcd = product.lib.gpqhe_spec_dcd_taken()
+    assert mismatches(want, got) == []
+    assert dcd >= 5, dcd
+
+
 def test_rekey_between_speculative_steps(oracle, product):
     """The speculative ModUp is keyed on the public key's block (api.cpp
     SpecModup / C1Prov): re-keying between steps -- the key freed and a new
@@ -667,7 +688,7 @@ def test_rekey_between_speculative_steps(oracle, product):
 
 @pytest.mark.parametrize("switch", ["GPQHE_SPEC", "GPQHE_SPEC_ATTACH", "GPQHE_SPEC_EARLY", "GPQHE_DEFER",
                                     "GPQHE_DEFER_SUB", "GPQHE_DEFER_GEMV", "GPQHE_SPEC_ATTACH_TAKE",
-                                    "GPQHE_SPEC_GEMV", "GPQHE_SPEC_MODUP_SPLIT"])
+                                    "GPQHE_SPEC_GEMV", "GPQHE_SPEC_MODUP_SPLIT", "GPQHE_SPEC_DCD"])
 def test_small_n_switch_off_paths(switch):
     """Each small-N switch is read once per process (api.cpp static const), so
     its off path runs in a child process (one at a time, nothing else on the
