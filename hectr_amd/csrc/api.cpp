@@ -532,6 +532,8 @@ static void sd_replay(const SdPat &r)
   }
   const size_t zb = (size_t)r.slots * 16;
   if (g_sd.zbytes < zb) {
+    if (g_sd.ev)
+      HIP_CHECK(hipEventSynchronize(g_sd.ev));  // (an earlier replay may still write it)
     if (g_sd.z)
       HIP_CHECK(hipHostFree(g_sd.z));
     HIP_CHECK(hipHostMalloc(&g_sd.z, zb, hipHostMallocDefault));
