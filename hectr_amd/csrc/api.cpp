@@ -1360,6 +1360,8 @@ static void flush_pending()
   std::vector<int64_t> vals;
   ecd.swap(g_pecd);
   enc.swap(g_penc);
+  if (!ecd.empty() || !enc.empty())
+    g_sd.valid = false;  // (its outputs may take blocks the replayed tail read: SpecDcd)
   vals.swap(g_pcoef);
   const size_t n = G.n;
   // an encoding of s slots is zero off the stride n / 2s: the launches take
@@ -2543,6 +2545,7 @@ static void flush_gemvs()
   q.swap(g_pgemv);
   if (q.empty())
     return;
+  g_sd.valid = false;  // (its outputs may take blocks the replayed tail read: SpecDcd)
   const unsigned k = (unsigned)q.size(), lvl = q[0].lvl;
   const unsigned nm = lvl + G.K, ndig = (lvl + G.alpha - 1) / G.alpha;
   const size_t n = G.n;

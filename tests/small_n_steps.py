@@ -202,6 +202,15 @@ def speculative_gemvs(e, seed=1234, rng_seed=53, plan=None):
         elif kind == "one":
             e.gemv(ya, Ma.ravel(), xd, rk)
             e.copy_ct(yb, ya)
+        elif kind == "realias":
+            # the speculated result freed and its block (likely) handed to a
+            # gemv that is not speculated (another matrix), whose queued launch
+            # writes it before the tail reads it (SpecDcd must not replay)
+            e.gemv(ya, Ma.ravel(), xd, rk)
+            e.gemv(yb, M2.ravel(), ud, rk)
+            e.free(ya)
+            ya = e.ct()
+            e.gemv(ya, M3.ravel(), ud, rk)
         else:
             e.gemv(ya, Ma.ravel(), xd, rk)
             e.gemv(yb, M2.ravel(), ud, rk)

@@ -660,12 +660,13 @@ def test_speculative_decode(oracle, product, monkeypatch):
     elementwise program and decode on this step's speculated gemvs): runs of
     HECTR's step in its own call order, broken by steps whose program or
     operands differ (a changed matrix, an encryption overwritten before its
-    he_sub, the gemvs in the other order, one gemv), where the replay must not
+    he_sub, the gemvs in the other order, one gemv, a speculated result's
+    block handed to a gemv that is not speculated), where the replay must not
     be taken -- every decoded value and object bit-exact vs the oracle, and the
     product served decodes from the replay."""
     from tests.small_n_steps import mismatches, speculative_gemvs
     plan = ["same"] * 7 + ["newM", "same", "same", "same", "clobber"] + ["same"] * 4 + ["order"] + ["same"] * 4 + \
-        ["one"] + ["same"] * 4
+        ["one"] + ["same"] * 4 + ["realias"] + ["same"] * 4
     # (a Python caller outruns the device: keep the replay on, which the
     # library otherwise stops after two late steps)
     monkeypatch.setenv("GPQHE_SPEC_DCD", "2")
