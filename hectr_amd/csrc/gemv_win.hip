@@ -1084,7 +1084,7 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
     HIP_CHECK(hipMemsetAsync(acc, 0, (size_t)cnt * as * 8, G.stream));
   const unsigned keep = mode == 1 ? lvl - 1 : lvl, nd = nm - keep;
   const bool fused = k_ks_fused_ok() && nd <= 5;
-  bool pre = false;
+  bool pre = false, s79 = false;
   if (fused) {
     LimbSet dr{};
     dr.base = acc + ((size_t)keep << logn);
@@ -1095,13 +1095,20 @@ static void gemv_chunk(uint64_t *y, size_t y_stride, size_t y_pstride, const uin
       dr.mods[d] = (uint8_t)(keep + d < lvl ? keep + d : G.L + (keep + d - lvl));
     // the ModDown scale on the row pass's output, so dn_cols runs its
     // pre-scaled (staged-constant) form
-    pre = k_ntt_rows_down(dr, lvl, mode);
-    if (!pre)
+    // (n = 2^16: on 512-element rows, so the ModDown's column kernels run
+    // their T = 128 forms, as the split key switch's: GPQHE_DN_S79=0 keeps
+    // 256 x 256)
+    const char *sw = getenv("GPQHE_DN_S79");
+    s79 = logn == 16 && !(sw && atoi(sw) == 0);
+    pre = k_ntt_rows_down(dr, lvl, mode, s79);
+    if (!pre) {
+      s79 = false;
       k_ntt_rows(dr, dr, true);
+    }
   }
   auto down = [&](uint64_t *o, uint64_t *X, unsigned npoly) {
     if (fused)
-      k_moddown_fused(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode, pre);
+      k_moddown_fused(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode, pre, s79);
     else
       k_moddown(o, y_pstride, X, (size_t)nm * n, npoly, lvl, mode);
   };

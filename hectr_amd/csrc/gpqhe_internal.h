@@ -461,9 +461,12 @@ void k_mul_relin_split(uint64_t *out, size_t out_pstride, const uint64_t *a, con
 // keep).
 // pre: the drop limbs' row pass also applied n^-1 [(D/d)^-1]_d
 // (k_ntt_rows_down), so the pre-scaled column kernels run.
+// s79 (n = 2^16): the drop limbs' row pass ran on 512-element rows
+// (k_ntt_rows_down with s79), so the 128 x 512 tiling follows, as the split
+// key switch's; otherwise k_ntt_ex's 256 x 256.
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly,
-                     unsigned lvl, int mode, bool pre = false);
-bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode);
+                     unsigned lvl, int mode, bool pre = false, bool s79 = false);
+bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode, bool s79 = false);
 bool k_prof_on();
 void k_prof_release();
 // Live kernel statistics (gpqhe_prof_enable): HIP events around one launch

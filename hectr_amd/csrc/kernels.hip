@@ -3938,7 +3938,7 @@ static void dn_fused_launch(uint64_t *conv, uint64_t *out, size_t out_pstride, c
 // takes the pre-scaled column kernels (pre = true), as the split key switch's
 // dropped slots do.  False (nothing launched) when the batched row form does
 // not apply: then k_ntt_rows and pre = false.
-bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode)
+bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode, bool s79)
 {
   const char *sw = getenv("GPQHE_DN_PRE");  // (read per call: tests switch it in-process)
   const bool on = !(sw && atoi(sw) == 0);
@@ -3952,7 +3952,7 @@ bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode)
     case 13: ok = ntt_rows_launch<7>(true, dr, dr, tab.ysc); break;
     case 14: ok = ntt_rows_launch<7>(true, dr, dr, tab.ysc); break;
     case 15: ok = ntt_rows_launch<8>(true, dr, dr, tab.ysc); break;
-    case 16: ok = ntt_rows_launch<8>(true, dr, dr, tab.ysc); break;
+    case 16: ok = s79 ? ntt_rows_launch<9>(true, dr, dr, tab.ysc) : ntt_rows_launch<8>(true, dr, dr, tab.ysc); break;
     case 17: ok = ntt_rows_launch<9>(true, dr, dr, tab.ysc); break;
     default: ok = false;
     }
@@ -3962,7 +3962,7 @@ bool k_ntt_rows_down(const LimbSet &dr, unsigned lvl, int mode)
 }
 
 void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_pstride, unsigned npoly, unsigned lvl,
-                     int mode, bool pre)
+                     int mode, bool pre, bool s79)
 {
   if (mode != 0 && mode != 1)
     gpqhe_die("fused ModDown: mode %d", mode);
@@ -3974,7 +3974,12 @@ void k_moddown_fused(uint64_t *out, size_t out_pstride, uint64_t *X, size_t x_ps
   case 13: dn_fused_launch<6, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
   case 14: dn_fused_launch<7, 7>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
   case 15: dn_fused_launch<7, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
-  case 16: dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
+  case 16:
+    if (s79)  // (the split key switch's 128 x 512 tiling: the column kernels' T = 128 forms)
+      dn_fused_launch<7, 9>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre);
+    else
+      dn_fused_launch<8, 8>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre);
+    break;
   case 17: dn_fused_launch<8, 9>(conv, out, out_pstride, X, x_pstride, npoly, lvl, tab, pre); break;
   default: gpqhe_die("fused ModDown needs 2^13 <= n <= 2^17");
   }
