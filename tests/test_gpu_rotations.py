@@ -179,12 +179,14 @@ def test_gemv_batch_few_diagonals(oracle, product, name, diags):
         e.free_evks(k[2])
 
 
+@pytest.mark.parametrize("switch", ["GPQHE_DN_PRE", "GPQHE_DN_S79"])
 @pytest.mark.parametrize("name", ["bench51", "bench_d2"])
-def test_gemv_rot_batch_dn_pre_off(oracle, product, monkeypatch, name):
+def test_gemv_rot_batch_dn_pre_off(oracle, product, monkeypatch, name, switch):
     """GPQHE_DN_PRE=0: the ModDown of he_gemv_batch / he_rot_batch on the
     generic column kernel with the scale after its inverse column pass,
-    instead of the pre-scaled row pass + dn_colsf form -- the
-    same residues as the oracle either way."""
+    instead of the pre-scaled row pass + dn_colsf form; GPQHE_DN_S79=0: the
+    pre-scaled form on the 256 x 256 tiling instead of 128 x 512
+    -- the same residues as the oracle either way."""
     init_slots(oracle, product, name, 16, seed=43)
     s, n, lvl, cnt = 16, product.n, 8, 3
     ko, kp = rot_keys(oracle), rot_keys(product)
@@ -192,7 +194,7 @@ def test_gemv_rot_batch_dn_pre_off(oracle, product, monkeypatch, name):
     zs = rng.uniform(-1, 1, (cnt, s)) + 1j * rng.uniform(-1, 1, (cnt, s))
     Mc = np.ascontiguousarray(sample_matrix(s, 5).ravel(), dtype=np.complex128)
     host = encrypt_batch(product, kp[0], zs, nlimbs=lvl)
-    monkeypatch.setenv("GPQHE_DN_PRE", "0")
+    monkeypatch.setenv(switch, "0")
     want, got = run_batch(oracle, product, ko[2], kp[2], "he_gemv_batch", host, cnt * 2 * (lvl - 1) * n,
                           Mc.ctypes.data, "IN", cnt, lvl)
     assert np.array_equal(got, want), f"gemv: {np.count_nonzero(got != want)} residues differ"
